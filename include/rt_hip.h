@@ -1,0 +1,71 @@
+/* rt_hip.h — C ABI of the gfx950 render path (librtc_amd.so).
+ *
+ * Boundary it replaces: the body of `void Camera_render(const Camera*, const World*, uint8_t*)`
+ * (reference include/raytracing.h:41, src/raytracing.c:86-135).  The reference's only FFI-style
+ * seam is that function; the library keeps its symbol (include/raytracing.h) and implements it as
+ *     rt_flatten(camera, world)  ->  rt_render(flat, n_gpus, buffer)
+ * The lower-level entry points below let a host in any language (ctypes, cgo, JNI: INTEGRATION.md)
+ * drive the same kernel with device-resident buffers and its own streams.
+ *
+ * Conventions: plain C types only, int status (0 = ok, <0 = error, message via rt_last_error()),
+ * no torch or HIP types in signatures (streams are passed as void* hipStream_t).
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include "rt_flat.h"
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef struct Camera Camera;
+typedef struct World World;
+typedef struct rt_device_scene rt_device_scene; /* opaque: scene arrays resident in one GPU's HBM */
+
+/* ---- host side: World graph -> flat arrays (replaces the pointer walk of src/raytracing.c:39-84) */
+rt_flat_scene *rt_flatten(const Camera *camera, const World *world);
+void rt_flat_free(rt_flat_scene *scene);
+
+/* ---- scene presets: the reference driver's scenes 0..7 (src/main.c:9-273, numbering of
+ * src/main.c:294-329), built by this library with the reference's defaults (src/main.c:278-287);
+ * width <= 0 / spp <= 0 / max_depth <= 0 keep the default (500 / 100 / 50). */
+rt_flat_scene *rt_scene_preset(int scene_id, int width, int spp, int max_depth);
+
+/* ---- device side -------------------------------------------------------------------------- */
+int rt_device_count(void);
+/* Copy `scene` into HBM of `device` (synchronous, once per render). */
+rt_device_scene *rt_scene_upload(const rt_flat_scene *scene, int device);
+void rt_scene_release(rt_device_scene *dscene);
+
+/* Render rows row0, row0 + row_stride, ... (n_rows of them) into d_out (device pointer,
+ * n_rows * width * 3 bytes, compact, in that row order).  Asynchronous on `stream`
+ * (hipStream_t, NULL = default stream of the scene's device).  This is the hot path. */
+int rt_render_rows_async(rt_device_scene *dscene, int row0, int row_stride, int n_rows, uint8_t *d_out,
+                         void *stream);
+
+/* Whole frame into a host buffer (width*height*3), rows interleaved j mod n_gpus over GPUs
+ * 0..n_gpus-1 (n_gpus <= 0: all visible), one host thread + stream per GPU, no collectives.
+ * Synchronous.  This is what Camera_render calls. */
+int rt_render(const rt_flat_scene *scene, int n_gpus, uint8_t *out_host);
+
+/* Kernel-side timing of the last rt_render call on `device`: milliseconds between HIP events
+ * bracketing its kernel launches (excludes upload and D2H). */
+double rt_last_kernel_ms(int device);
+
+/* Diagnostics: evaluate the device libm port (rt_libm.h) on n inputs.
+ * fn: 0 = sincosf (out[2i] = sin, out[2i+1] = cos), 1 = powf(x, 5), 2 = logf, 3 = sinf. */
+int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device);
+
+const char *rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */

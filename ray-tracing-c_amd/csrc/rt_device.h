@@ -1,0 +1,628 @@
+// rt_device.h — gfx950 device code of the hot path: one ray-colour loop per pixel lane.
+//
+// Reference hot path (ray-tracing-c @ v2), re-expressed for a 64-wide wavefront:
+//   Camera_render       src/raytracing.c:86-135  -> rt_render_pixel   (rt_kernel.hip)
+//   Camera_ray_color    src/raytracing.c:39-84   -> rt_path           (iterative, explicit fold)
+//   HittableList/BVH/Sphere/Quad/Translate/RotateY/ConstantMedium hit
+//                       src/hittable.c:38-423    -> rt_trace          (explicit-stack DFS)
+//   Material_*          src/material.c:23-152    -> rt_scatter / rt_emit / rt_scatter_pdf
+//   Texture value       src/texture.c:8-114      -> rt_texture_value
+//   pcg32               src/pcg32.c:3-22         -> Pcg32
+//   vec3                src/vec3.c               -> f3 helpers below (same operation order)
+//
+// Bit-exactness rules:
+//  * build with -ffp-contract=off, IEEE div/sqrt (hipcc default correctly-rounded f32 div/sqrt),
+//    denormals on;  every expression below keeps the reference's association order;
+//  * rng draws happen in the gcc-built reference's order (right-to-left argument evaluation);
+//  * traversal visits objects in the reference's order with the same shrinking t_max;
+//  * the recursive colour `e + a * color(next) [* w]` is folded innermost-first from a per-lane
+//    record of (e, a, w) so rounding equals the recursion's;
+//  * glibc transcendentals come from rt_libm.h (bit-exact ports).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_flat.h"
+#include "rt_libm.h"
+
+#define RT_D __device__ __forceinline__
+
+namespace rt {
+
+constexpr float kPi = 3.14159265358979323846f;      // (float)M_PI
+constexpr float kInvPi = 0.318309886183790671538f;  // (float)M_1_PI
+constexpr int kStackMax = 48;                       // DFS stack slots (flattener checks need <= this)
+constexpr int kMaxDepth = 64;                       // path record slots (host checks max_depth)
+
+// ------------------------------------------------------------------------------ vectors
+struct f3 {
+  float x, y, z;
+};
+RT_D f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+RT_D f3 ld3(const float *p) { return f3{p[0], p[1], p[2]}; }
+RT_D f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_D f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_D f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_D f3 scale(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+RT_D f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+RT_D float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+RT_D f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
+RT_D f3 normalize(f3 a) { return scale(a, 1.0f / sqrtf(dot(a, a))); }  // vec3_div(u, |u|)
+RT_D f3 ray_at(f3 o, f3 d, float t) { return add(o, scale(d, t)); }
+
+// ------------------------------------------------------------------------------ pcg32
+struct Pcg32 {
+  uint64_t state, inc;
+  RT_D uint32_t next() {
+    const uint64_t s = state;
+    state = s * 6364136223846793005ULL + inc;
+    const uint32_t x = (uint32_t)(((s >> 18u) ^ s) >> 27u);
+    return __builtin_rotateright32(x, (uint32_t)(s >> 59u));
+  }
+  RT_D void seed(uint64_t initstate, uint64_t initseq) {
+    state = 0u;
+    inc = (initseq << 1u) | 1u;
+    (void)next();
+    state += initstate;
+    (void)next();
+  }
+  RT_D float f32() { return (float)(next() >> 8) * 0x1p-24f; }  // == (float)(u>>8) / 2^24
+  RT_D float between(float lo, float hi) { return lo + f32() * (hi - lo); }
+};
+
+// vec3_rand_between in gcc order: z first, then y, then x (src/vec3.c:33-35)
+RT_D f3 rand_between(Pcg32 &g, float lo, float hi) {
+  const float z = g.between(lo, hi);
+  const float y = g.between(lo, hi);
+  const float x = g.between(lo, hi);
+  return mk(x, y, z);
+}
+RT_D f3 rand_unit_vector(Pcg32 &g) {  // src/vec3.c:36-43
+  for (;;) {
+    const f3 c = rand_between(g, -1.0f, 1.0f);
+    const float l2 = dot(c, c);
+    if (l2 < 1.0f) return scale(c, 1.0f / sqrtf(l2));
+  }
+}
+
+// ------------------------------------------------------------------------------ scene view
+struct DScene {
+  rt_camera cam;
+  int32_t root, lights, features, pad;
+  const rt_bvh_node *bvh;
+  const rt_sphere *spheres;
+  const rt_quad *quads;
+  const rt_list *lists;
+  const int32_t *items;
+  const rt_translate *translates;
+  const rt_rotate_y *rotates;
+  const rt_medium *media;
+  const rt_material *materials;
+  const rt_texture *textures;
+  const rt_image *images;
+  const rt_perlin *perlins;
+  const uint8_t *image_bytes;
+  int32_t n_textures, n_images;
+};
+
+// ------------------------------------------------------------------------------ primitives
+// Sphere_hit up to the accepted root (src/hittable.c:120-138); a = |d|^2 hoisted per ray.
+RT_D bool sphere_t(const rt_sphere &s, f3 o, f3 d, float a, float tmin, float tmax, float &t) {
+  const f3 oc = sub(o, ld3(s.center));
+  const float b = dot(oc, d);
+  const float c = dot(oc, oc) - s.radius_sq;
+  const float disc = b * b - a * c;
+  if (disc < 0) return false;
+  const float sq = sqrtf(disc);
+  float root = (-b - sq) / a;
+  if (root <= tmin || root >= tmax) {
+    root = (-b + sq) / a;
+    if (root <= tmin || root >= tmax) return false;
+  }
+  t = root;
+  return true;
+}
+
+// Quad_hit up to acceptance (src/hittable.c:186-203); note the INCLUSIVE t range.
+RT_D bool quad_t(const rt_quad &q, f3 o, f3 d, float tmin, float tmax, float &t) {
+  const f3 n = ld3(q.normal);
+  const float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  const float tt = (q.D - dot(n, o)) / denom;
+  if ((tt < tmin) || (tt > tmax)) return false;
+  const f3 hp = sub(ray_at(o, d, tt), ld3(q.Q));
+  const f3 w = ld3(q.w);
+  const float alpha = dot(w, cross(hp, ld3(q.v)));
+  const float beta = dot(w, cross(ld3(q.u), hp));
+  if ((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1)) return false;
+  t = tt;
+  return true;
+}
+
+RT_D bool prim_t(const DScene &S, int32_t ref, f3 o, f3 d, float tmin, float tmax, float &t) {
+  const int32_t i = rt_ref_index(ref);
+  if (rt_ref_kind(ref) == RT_KIND_SPHERE) return sphere_t(S.spheres[i], o, d, dot(d, d), tmin, tmax, t);
+  return quad_t(S.quads[i], o, d, tmin, tmax, t);
+}
+
+// AABB_hit (src/hittable.c:38-55) with 1/d hoisted per ray (same division, same value).
+RT_D bool aabb_hit(const rt_bvh_node &n, f3 o, f3 inv, float tmin, float tmax) {
+  const float lo[3] = {n.lo[0], n.lo[1], n.lo[2]};
+  const float hi[3] = {n.hi[0], n.hi[1], n.hi[2]};
+  const float oo[3] = {o.x, o.y, o.z};
+  const float iv[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    float t0 = (lo[a] - oo[a]) * iv[a];
+    float t1 = (hi[a] - oo[a]) * iv[a];
+    if (iv[a] < 0) {
+      const float s = t0;
+      t0 = t1;
+      t1 = s;
+    }
+    tmin = fmaxf(tmin, t0);
+    tmax = fminf(tmax, t1);
+    if (tmax <= tmin) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------------------ transforms
+RT_D f3 rot_y(f3 u, float c, float s) { return mk(c * u.x - s * u.z, u.y, s * u.x + c * u.z); }
+RT_D f3 rot_y_inv(f3 u, float c, float s) { return mk(c * u.x + s * u.z, u.y, -s * u.x + c * u.z); }
+
+// Ray in the frame of transform `xf` (a TRANSLATE / ROTATE_Y ref, or NONE = world):
+// apply the chain outermost first, exactly as nested Translate_hit / RotateY_hit do.
+RT_D void local_ray(const DScene &S, int32_t xf, f3 wo, f3 wd, f3 &o, f3 &d) {
+  int32_t chain[8];
+  int n = 0;
+  while (xf != RT_REF_NONE && n < 8) {
+    chain[n++] = xf;
+    xf = rt_ref_kind(xf) == RT_KIND_TRANSLATE ? S.translates[rt_ref_index(xf)].parent_xform
+                                               : S.rotates[rt_ref_index(xf)].parent_xform;
+  }
+  o = wo;
+  d = wd;
+  for (int k = n - 1; k >= 0; k--) {
+    const int32_t r = chain[k];
+    if (rt_ref_kind(r) == RT_KIND_TRANSLATE) {
+      o = sub(o, ld3(S.translates[rt_ref_index(r)].offset));
+    } else {
+      const rt_rotate_y &ry = S.rotates[rt_ref_index(r)];
+      o = rot_y(o, ry.cos_theta, ry.sin_theta);
+      d = rot_y(d, ry.cos_theta, ry.sin_theta);
+    }
+  }
+}
+
+RT_D int32_t parent_of(const DScene &S, int32_t xf) {
+  return rt_ref_kind(xf) == RT_KIND_TRANSLATE ? S.translates[rt_ref_index(xf)].parent_xform
+                                               : S.rotates[rt_ref_index(xf)].parent_xform;
+}
+
+// ------------------------------------------------------------------------------ traversal
+struct Hit {
+  float t;
+  int32_t prim;   // winning SPHERE / QUAD / MEDIUM ref
+  int32_t xform;  // transform frame the winner was hit in (NONE = world)
+};
+
+// Closest hit over World.objects in [tmin, inf): the reference's recursive visit order
+// (lists in order, BVH node box -> left -> right with t_max = closest so far) as an explicit DFS.
+// Exit markers restore the parent frame after a transform's subtree.
+constexpr int32_t kExitTag = 7;
+
+template <int F>
+RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
+  // entry = ref | (list cursor position << 32); lists are walked through a cursor entry so a list
+  // of any length costs one stack slot (need computed by rt_flatten.c: stack_need)
+  uint64_t stack[kStackMax];
+  int sp = 0;
+  stack[sp++] = (uint32_t)S.root;
+  float tmax = __builtin_inff();
+  bool found = false;
+  int32_t frame = RT_REF_NONE;
+  f3 o = wo, d = wd;
+  f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float dd = dot(d, d);
+  while (sp > 0) {
+    const uint64_t e = stack[--sp];
+    const int32_t ref = (int32_t)(uint32_t)e;
+    const int kind = rt_ref_kind(ref);
+    const int32_t idx = rt_ref_index(ref);
+    if ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) {
+      const rt_bvh_node &n = S.bvh[idx];
+      if (aabb_hit(n, o, inv, tmin, tmax)) {
+        if (n.right != RT_REF_NONE) stack[sp++] = (uint32_t)n.right;
+        stack[sp++] = (uint32_t)n.left;
+      }
+    } else if (kind == RT_KIND_SPHERE) {
+      float t;
+      if (sphere_t(S.spheres[idx], o, d, dd, tmin, tmax, t)) {
+        tmax = t;
+        h.t = t;
+        h.prim = ref;
+        h.xform = frame;
+        found = true;
+      }
+    } else if (kind == RT_KIND_LIST) {
+      const rt_list l = S.lists[idx];
+      const int32_t pos = (int32_t)(e >> 32);
+      if (pos < l.count) {
+        if (pos + 1 < l.count) stack[sp++] = (uint32_t)ref | ((uint64_t)(pos + 1) << 32);
+        stack[sp++] = (uint32_t)S.items[l.first + pos];
+      }
+    } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
+      float t;
+      if (quad_t(S.quads[idx], o, d, tmin, tmax, t)) {
+        tmax = t;
+        h.t = t;
+        h.prim = ref;
+        h.xform = frame;
+        found = true;
+      }
+    } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
+      stack[sp++] = (uint32_t)rt_ref(kExitTag, 0) | ((uint64_t)(uint32_t)ref << 32);
+      stack[sp++] = (uint32_t)(kind == RT_KIND_TRANSLATE ? S.translates[idx].child : S.rotates[idx].child);
+      frame = ref;
+      local_ray(S, frame, wo, wd, o, d);
+      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      dd = dot(d, d);
+    } else if ((F & RT_FEAT_XFORM) && kind == kExitTag) {
+      frame = parent_of(S, (int32_t)(uint32_t)(e >> 32));
+      local_ray(S, frame, wo, wd, o, d);
+      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      dd = dot(d, d);
+    } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
+      // ConstantMedium_hit (src/hittable.c:392-423): two boundary hits, clamp, one rng draw
+      const rt_medium m = S.media[idx];
+      float t1, t2;
+      if (prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
+          prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2)) {
+        t1 = fmaxf(t1, tmin);
+        t2 = fminf(t2, tmax);
+        if (!(t1 >= t2)) {
+          t1 = t1 > 0.0f ? t1 : 0.0f;
+          const float len = sqrtf(dd);
+          const float inside = (t2 - t1) * len;
+          const float dist = m.neg_inv_density * rtm::logf(g.f32());
+          if (!(dist > inside)) {
+            const float t = t1 + dist / len;
+            tmax = t;
+            h.t = t;
+            h.prim = ref;
+            h.xform = frame;
+            found = true;
+          }
+        }
+      }
+    }
+  }
+  return found;
+}
+
+// ------------------------------------------------------------------------------ hit record
+struct Rec {
+  f3 p, normal;
+  float u, v;
+  int32_t material;
+  bool front;
+};
+
+// Rebuild the winner's HitRecord exactly as its hit() wrote it, then apply the enclosing
+// transforms' fix-ups innermost-first (RotateY_hit / Translate_hit post-processing).
+template <int F>
+RT_D void make_record(const DScene &S, f3 wo, f3 wd, const Hit &h, Rec &r) {
+  f3 o = wo, d = wd;
+  if ((F & RT_FEAT_XFORM) && h.xform != RT_REF_NONE) local_ray(S, h.xform, wo, wd, o, d);
+  const int kind = rt_ref_kind(h.prim);
+  const int32_t idx = rt_ref_index(h.prim);
+  r.p = ray_at(o, d, h.t);
+  r.u = r.v = 0.0f;
+  r.front = true;
+  r.normal = mk(0.0f, 0.0f, 0.0f);
+  if (kind == RT_KIND_SPHERE) {
+    const rt_sphere &s = S.spheres[idx];
+    const f3 outward = scale(sub(r.p, ld3(s.center)), s.inv_radius);
+    r.front = dot(d, outward) < 0.0f;
+    r.normal = r.front ? outward : neg(outward);
+    if (F & RT_FEAT_TEX_UV) {
+      r.u = (atan2f(-outward.z, outward.x) + kPi) * kInvPi * 0.5f;
+      r.v = acosf(-outward.y) * kInvPi;
+    }
+    r.material = s.material;
+  } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
+    const rt_quad &q = S.quads[idx];
+    const f3 hp = sub(r.p, ld3(q.Q));
+    const f3 w = ld3(q.w);
+    r.u = dot(w, cross(hp, ld3(q.v)));
+    r.v = dot(w, cross(ld3(q.u), hp));
+    const f3 n = ld3(q.normal);
+    r.front = dot(d, n) < 0.0f;
+    r.normal = r.front ? n : neg(n);
+    r.material = q.material;
+  } else {  // medium: normal / front / u / v are stale in the reference and unused by Isotropic
+    r.material = S.media[idx].phase_material;
+  }
+  if ((F & RT_FEAT_XFORM) && h.xform != RT_REF_NONE) {
+    for (int32_t xf = h.xform; xf != RT_REF_NONE; xf = parent_of(S, xf)) {
+      if (rt_ref_kind(xf) == RT_KIND_ROTATE_Y) {
+        const rt_rotate_y &ry = S.rotates[rt_ref_index(xf)];
+        r.p = rot_y_inv(r.p, ry.cos_theta, ry.sin_theta);
+        r.normal = rot_y_inv(r.normal, ry.cos_theta, ry.sin_theta);
+      } else {
+        r.p = add(r.p, ld3(S.translates[rt_ref_index(xf)].offset));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ textures
+RT_D float perlin_noise(const rt_perlin &P, f3 p) {  // src/texture.c:78-103
+  const int i = (int)floorf(p.x), j = (int)floorf(p.y), k = (int)floorf(p.z);
+  const float t1 = p.x - (float)i, t2 = p.y - (float)j, t3 = p.z - (float)k;
+  const float s1 = t1 * t1 * (3.0f - 2.0f * t1);
+  const float s2 = t2 * t2 * (3.0f - 2.0f * t2);
+  const float s3 = t3 * t3 * (3.0f - 2.0f * t3);
+  float value = 0;
+  for (int di = 0; di < 2; di++)
+    for (int dj = 0; dj < 2; dj++)
+      for (int dk = 0; dk < 2; dk++) {
+        const int gi = P.perm_x[(i + di) & 255] ^ P.perm_y[(j + dj) & 255] ^ P.perm_z[(k + dk) & 255];
+        const f3 grad = mk(P.grad[gi][0], P.grad[gi][1], P.grad[gi][2]);
+        const f3 wgt = mk(t1 - (float)di, t2 - (float)dj, t3 - (float)dk);
+        value += dot(grad, wgt) * ((float)di * s1 + (float)(1 - di) * (1.0f - s1)) *
+                 ((float)dj * s2 + (float)(1 - dj) * (1.0f - s2)) * ((float)dk * s3 + (float)(1 - dk) * (1.0f - s3));
+      }
+  return value;
+}
+
+RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p) {
+  for (int hops = 0; hops < 16; hops++) {
+    const rt_texture &t = S.textures[tex];
+    if (t.kind == RT_TEX_SOLID) return ld3(t.color);
+    if (t.kind == RT_TEX_CHECKER) {  // src/texture.c:12-22
+      const int iu = (int)floorf(u / t.scale);
+      const int iv = (int)floorf(v / t.scale);
+      tex = ((iu + iv) % 2) ? t.b : t.a;
+      continue;
+    }
+    if (t.kind == RT_TEX_IMAGE) {  // src/texture.c:28-37
+      const rt_image im = S.images[t.a];
+      int i = (int)roundf(u * (float)(im.width - 1));
+      int j = (int)roundf((1.0f - v) * (float)(im.height - 1));
+      i = min(max(i, 0), im.width - 1);  // memory safety only: in range for u,v in [0,1]
+      j = min(max(j, 0), im.height - 1);
+      const uint8_t *px = S.image_bytes + im.offset + ((int64_t)j * im.width + i) * 3;
+      return mk((float)px[0] / 255.0f, (float)px[1] / 255.0f, (float)px[2] / 255.0f);
+    }
+    // PERLIN: marble (src/texture.c:47-52, :105-114)
+    const rt_perlin &P = S.perlins[t.a];
+    f3 q = scale(p, t.scale);
+    const f3 q0 = q;
+    float acc = 0.0f, weight = 1.0f;
+    for (int o = 0; o < P.depth; o++) {
+      acc += weight * perlin_noise(P, q);
+      weight *= 0.5f;
+      q = scale(q, 2.0f);
+    }
+    const float value = 0.5f * (1.0f + rtm::sinf(q0.z + 10.0f * fabsf(acc)));
+    return mk(value, value, value);
+  }
+  return mk(0.0f, 0.0f, 0.0f);
+}
+
+// ------------------------------------------------------------------------------ materials
+struct Onb {
+  f3 u, v, w;
+};
+RT_D Onb onb_from_w(f3 n) {  // src/material.c:147-152
+  Onb b;
+  b.w = normalize(n);
+  const f3 a = fabsf(b.w.x) > 0.9f ? mk(0, 1, 0) : mk(1, 0, 0);
+  b.v = normalize(cross(b.w, a));
+  b.u = cross(b.w, b.v);
+  return b;
+}
+RT_D f3 onb_local(const Onb &b, f3 a) { return add(add(scale(b.u, a.x), scale(b.v, a.y)), scale(b.w, a.z)); }
+RT_D f3 reflect(f3 v, f3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
+
+template <int F>
+RT_D f3 emit(const DScene &S, const Rec &r) {  // Material_emit, src/material.c:133-142
+  if (F & RT_FEAT_EMISSIVE) {
+    const rt_material &m = S.materials[r.material];
+    if (m.tag == RT_MAT_SURFACE_NORMAL) return scale(add(r.normal, mk(1.0f, 1.0f, 1.0f)), 0.5f);
+    if (m.tag == RT_MAT_DIFFUSE_LIGHT && r.front) return texture_value(S, m.texture, r.u, r.v, r.p);
+  }
+  return mk(0.0f, 0.0f, 0.0f);
+}
+
+// Material_scatter (src/material.c:103-120).  Returns false when the path ends at this hit.
+template <int F>
+RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 &albedo, bool &skip_pdf) {
+  const rt_material &m = S.materials[r.material];
+  switch (m.tag) {
+  case RT_MAT_LAMBERTIAN: {  // src/material.c:23-37
+    const Onb b = onb_from_w(r.normal);
+    const float r1 = g.f32();
+    const float r2 = g.f32();
+    const float phi = (2.0f * kPi) * r1;
+    float sphi, cphi;
+    rtm::sincosf(phi, &sphi, &cphi);
+    const float sq = sqrtf(r2);
+    out = onb_local(b, mk(cphi * sq, sphi * sq, sqrtf(1.0f - r2)));
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    skip_pdf = false;
+    return true;
+  }
+  case RT_MAT_METAL: {  // src/material.c:48-58
+    const f3 refl = reflect(normalize(r_in), r.normal);
+    out = add(refl, scale(rand_unit_vector(g), m.param));
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    skip_pdf = true;
+    if (dot(out, r.normal) < 0.0f) out = refl;
+    return true;
+  }
+  case RT_MAT_DIELECTRIC: {  // src/material.c:62-86
+    float eta = m.param;
+    if (r.front) eta = 1.0f / eta;
+    const f3 v = normalize(r_in);
+    const float cos_t = fminf(-dot(v, r.normal), 1.0f);
+    const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+    float sch = (1.0f - eta) / (1.0f + eta);
+    sch *= sch;
+    sch += (1 - sch) * rtm::powf(1.0f - cos_t, 5.0f);
+    if (eta * sin_t > 1.0f || sch > g.f32()) {  // rng drawn only when not totally reflected
+      out = reflect(v, r.normal);
+    } else {
+      const f3 perp = scale(add(v, scale(r.normal, cos_t)), eta);
+      const f3 para = scale(r.normal, -sqrtf(fabsf(1.0f - dot(perp, perp))));
+      out = add(perp, para);
+    }
+    albedo = mk(1.0f, 1.0f, 1.0f);
+    skip_pdf = true;
+    return true;
+  }
+  case RT_MAT_ISOTROPIC: {  // src/material.c:93-98
+    out = rand_unit_vector(g);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    skip_pdf = false;
+    return true;
+  }
+  default:  // SURFACE_NORMAL, DIFFUSE_LIGHT
+    skip_pdf = true;
+    return false;
+  }
+}
+
+RT_D float scatter_pdf(const DScene &S, int32_t mat, f3 normal, f3 r_out) {  // src/material.c:122-131
+  const int tag = S.materials[mat].tag;
+  if (tag == RT_MAT_LAMBERTIAN) {
+    const float c = dot(normal, normalize(r_out));
+    return c < 0.0f ? 0.0f : c / kPi;
+  }
+  if (tag == RT_MAT_ISOTROPIC) return 1.0f / (4.0f * kPi);
+  return 0.0f;
+}
+
+// ------------------------------------------------------------------------------ light sampling
+// HittableList_rand over World.lights (src/hittable.c:101-107) + Sphere_rand / Quad_rand.
+RT_D f3 lights_rand(const DScene &S, f3 origin, Pcg32 &g) {
+  const rt_list L = S.lists[S.lights];
+  for (;;) {
+    const int32_t ref = S.items[L.first + (int32_t)(g.next() % (uint32_t)L.count)];
+    if (ref == RT_REF_NONE) continue;  // no rand(): rejection, as the reference recursion does
+    const int32_t i = rt_ref_index(ref);
+    if (rt_ref_kind(ref) == RT_KIND_QUAD) {  // src/hittable.c:225-228, gcc order: v gets draw 1
+      const rt_quad &q = S.quads[i];
+      const float fv = g.f32();
+      const float fu = g.f32();
+      return add(add(add(ld3(q.Q), scale(ld3(q.u), fu)), scale(ld3(q.v), fv)), neg(origin));
+    }
+    const rt_sphere &s = S.spheres[i];  // src/hittable.c:163-178
+    const f3 oc = sub(ld3(s.center), origin);
+    const float r1 = g.f32();
+    const float r2 = g.f32();
+    const float z = 1.0f + r2 * (sqrtf(1.0f - s.radius_sq / dot(oc, oc)) - 1);
+    const float phi = (2.0f * kPi) * r1;
+    float sphi, cphi;
+    rtm::sincosf(phi, &sphi, &cphi);
+    const float x = cphi * sqrtf(1.0f - z * z);
+    const float y = sphi * sqrtf(1.0f - z * z);
+    return onb_local(onb_from_w(oc), mk(x, y, z));
+  }
+}
+
+// HittableList_pdf over World.lights (src/hittable.c:89-100) + Sphere_pdf / Quad_pdf.
+RT_D float lights_pdf(const DScene &S, f3 o, f3 d) {
+  const rt_list L = S.lists[S.lights];
+  float pdf = 0.0f, count = 0.0f;
+  for (int k = 0; k < L.count; k++) {
+    const int32_t ref = S.items[L.first + k];
+    if (ref == RT_REF_NONE) continue;
+    const int32_t i = rt_ref_index(ref);
+    float val = 0.0f, t;
+    if (rt_ref_kind(ref) == RT_KIND_QUAD) {
+      const rt_quad &q = S.quads[i];
+      if (quad_t(q, o, d, 0.001f, __builtin_inff(), t)) {
+        const float d2 = t * t * dot(d, d);
+        const float c = fabsf(dot(ld3(q.normal), normalize(d)));
+        val = d2 / (c * q.area);
+      }
+    } else {
+      const rt_sphere &s = S.spheres[i];
+      if (sphere_t(s, o, d, dot(d, d), 0.001f, __builtin_inff(), t)) {
+        const f3 oc = sub(ld3(s.center), o);
+        const float ctm = sqrtf(1.0f - s.radius_sq / dot(oc, oc));
+        const float solid_angle = (2.0f * kPi) * (1.0f - ctm);
+        val = 1.0f / solid_angle;
+      }
+    }
+    pdf += val;
+    count += 1.0f;
+  }
+  return pdf / fmaxf(count, 1.0f);
+}
+
+// ------------------------------------------------------------------------------ one sample path
+// Camera_ray_color (src/raytracing.c:39-84) unrolled into a loop.  Each scattering bounce k
+// records (e_k, a_k, w_k); when the path ends with tail value c, the colour is folded
+// innermost-first: c = e_k + (a_k * c) [* w_k], which is the recursion's evaluation order.
+template <int F>
+RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
+  constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
+  f3 rec_a[kMaxDepth];
+  f3 rec_e[kFull ? kMaxDepth : 1];
+  float rec_w[kFull ? kMaxDepth : 1];
+  uint64_t weighted = 0;
+  int n = 0;
+  f3 tail;
+  const float prob = S.cam.light_prob;
+  for (int depth = S.cam.max_depth;; depth--) {
+    if (depth <= 0) {
+      tail = mk(0.0f, 0.0f, 0.0f);
+      break;
+    }
+    Hit h;
+    if (!trace<F>(S, o, d, 1e-3f, g, h)) {
+      tail = ld3(S.cam.background);
+      break;
+    }
+    Rec r;
+    make_record<F>(S, o, d, h, r);
+    const f3 e = emit<F>(S, r);
+    f3 out, albedo;
+    bool skip_pdf;
+    if (!scatter<F>(S, r, d, g, out, albedo, skip_pdf)) {
+      tail = e;
+      break;
+    }
+    rec_a[n] = albedo;
+    if (kFull) {
+      rec_e[n] = e;
+      if ((F & RT_FEAT_LIGHTS) && !skip_pdf) {  // mixture pdf (src/raytracing.c:61-71)
+        if (g.f32() < prob) out = lights_rand(S, r.p, g);
+        const float sp = scatter_pdf(S, r.material, r.normal, out);
+        const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, out);
+        rec_w[n] = sp / spdf;
+        weighted |= 1ull << n;
+      }
+    }
+    n++;
+    o = r.p;
+    d = out;
+  }
+  f3 c = tail;
+  for (int k = n - 1; k >= 0; k--) {
+    f3 x = mul(rec_a[k], c);
+    if (kFull) {
+      if ((weighted >> k) & 1) x = scale(x, rec_w[k]);
+      c = add(rec_e[k], x);
+    } else {
+      c = add(mk(0.0f, 0.0f, 0.0f), x);
+    }
+  }
+  return c;
+}
+
+}  // namespace rt

@@ -1,0 +1,404 @@
+// rt_kernel.hip — gfx950 render kernels + the C ABI declared in include/rt_hip.h.
+//
+// Work decomposition: one lane = one pixel (the reference's per-pixel pcg32 stream is sequential
+// across that pixel's samples, so pixels are the only parallel axis: SURVEY §0.6).  A launch
+// covers a set of image rows row0 + k*row_stride; multi-GPU runs give GPU g the rows j % G == g
+// (interleaved) and need no collective: each GPU writes its own compact rows.
+//
+// Kernel variants are compiled per feature set (rt_flat.h rt_feature_bits) so the Book-1 scenes
+// do not carry quad / transform / medium / light-sampling code.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_device.h"
+
+using namespace rt;
+
+// ------------------------------------------------------------------------------ errors
+static thread_local char g_err[1024];
+
+extern "C" void rt_set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+extern "C" const char *rt_last_error(void) { return g_err; }
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+#define HIP_OK(expr)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) {                                                                        \
+      rt_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);     \
+      return -1;                                                                                   \
+    }                                                                                              \
+  } while (0)
+
+// ------------------------------------------------------------------------------ kernels
+constexpr int kBlock = 256;
+constexpr int kFeatBook1 = RT_FEAT_BVH | RT_FEAT_DOF;  // spheres, lists, BVH: scenes 0 and 1
+constexpr int kFeatAll = 0x1ff;
+
+// Camera_render's per-pixel body (src/raytracing.c:93-131).
+template <int F>
+__global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int row0, int row_stride, int n_rows,
+                                                                uint8_t *__restrict__ out) {
+  const int W = S.cam.width;
+  const int64_t pix = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (pix >= (int64_t)n_rows * W) return;
+  const int jj = (int)(pix / W);
+  const int i = (int)(pix - (int64_t)jj * W);
+  const int j = row0 + jj * row_stride;
+
+  Pcg32 g;
+  g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));
+  const f3 du = ld3(S.cam.delta_u), dv = ld3(S.cam.delta_v), lf = ld3(S.cam.origin);
+  const f3 pixel_pos = add(add(ld3(S.cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+  const bool dof = S.cam.dof_angle > 0.0f;
+  f3 acc = mk(0.0f, 0.0f, 0.0f);
+  for (int s = 0; s < S.cam.spp; s++) {
+    const float px = g.between(-0.5f, 0.5f);
+    const float py = g.between(-0.5f, 0.5f);
+    f3 o = lf;
+    if (dof) {  // thin-lens disc by rejection (src/raytracing.c:108-117)
+      float a, b;
+      for (;;) {
+        a = g.between(-1.0f, 1.0f);
+        b = g.between(-1.0f, 1.0f);
+        if (a * a + b * b < 1.0f) break;
+      }
+      o = add(add(lf, scale(ld3(S.cam.disc_u), a)), scale(ld3(S.cam.disc_v), b));
+    }
+    const f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+    acc = add(acc, path_color<F>(S, o, d, g));
+  }
+  const float spp_f = (float)S.cam.spp;
+  const float ch[3] = {acc.x, acc.y, acc.z};
+  uint8_t *dst = out + pix * 3;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {  // gamma 2 + clamp macro semantics (NaN -> 0) + truncation
+    float v = sqrtf(ch[c] / spp_f);
+    v = v > 0.0f ? v : 0.0f;
+    v = v < 0.999f ? v : 0.999f;
+    dst[c] = (uint8_t)(int)(256.0f * v);
+  }
+}
+
+__global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float v = x[k];
+  if (fn == 0) {
+    float s, c;
+    rtm::sincosf(v, &s, &c);
+    out[2 * k] = s;
+    out[2 * k + 1] = c;
+  } else if (fn == 1) {
+    out[k] = rtm::powf(v, 5.0f);
+  } else if (fn == 2) {
+    out[k] = rtm::logf(v);
+  } else {
+    out[k] = rtm::sinf(v);
+  }
+}
+
+// ------------------------------------------------------------------------------ device scene
+struct rt_device_scene {
+  int device;
+  DScene view;
+  void *arena;
+  size_t arena_bytes;
+  int features;
+  int width, height;
+};
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static bool ref_ok(const rt_flat_scene *s, int32_t ref, bool allow_none) {
+  if (ref == RT_REF_NONE) return allow_none;
+  const int32_t i = rt_ref_index(ref);
+  switch (rt_ref_kind(ref)) {
+  case RT_KIND_BVH: return i < s->n_bvh;
+  case RT_KIND_SPHERE: return i < s->n_spheres;
+  case RT_KIND_QUAD: return i < s->n_quads;
+  case RT_KIND_LIST: return i < s->n_lists;
+  case RT_KIND_TRANSLATE: return i < s->n_translates;
+  case RT_KIND_ROTATE_Y: return i < s->n_rotates;
+  case RT_KIND_MEDIUM: return i < s->n_media;
+  default: return false;
+  }
+}
+
+// Every index the kernel will follow is checked here, so a malformed scene fails on the host
+// instead of faulting the GPU.
+static int validate(const rt_flat_scene *s) {
+  const rt_camera &c = s->camera;
+  if (c.width <= 0 || c.height <= 0 || c.spp <= 0) return rt_set_error("bad image size / spp"), -1;
+  if (c.max_depth > kMaxDepth)
+    return rt_set_error("max_depth %d exceeds the kernel's path record (%d)", c.max_depth, kMaxDepth), -1;
+  if (s->stack_needed > kStackMax)
+    return rt_set_error("scene needs %d traversal stack slots, kernel has %d", s->stack_needed, kStackMax), -1;
+  if (!ref_ok(s, s->root, false) || rt_ref_kind(s->root) != RT_KIND_LIST) return rt_set_error("bad root"), -1;
+  if (s->lights < 0 || s->lights >= s->n_lists) return rt_set_error("bad lights list"), -1;
+  for (int k = 0; k < s->n_bvh; k++)
+    if (!ref_ok(s, s->bvh[k].left, false) || !ref_ok(s, s->bvh[k].right, true)) return rt_set_error("bad bvh ref"), -1;
+  for (int k = 0; k < s->n_lists; k++)
+    if (s->lists[k].first < 0 || s->lists[k].count < 0 || s->lists[k].first + s->lists[k].count > s->n_list_items)
+      return rt_set_error("bad list range"), -1;
+  for (int k = 0; k < s->n_list_items; k++)
+    if (!ref_ok(s, s->list_items[k], true)) return rt_set_error("bad list item"), -1;
+  for (int k = 0; k < s->n_translates; k++)
+    if (!ref_ok(s, s->translates[k].child, false) || !ref_ok(s, s->translates[k].parent_xform, true))
+      return rt_set_error("bad translate"), -1;
+  for (int k = 0; k < s->n_rotates; k++)
+    if (!ref_ok(s, s->rotates[k].child, false) || !ref_ok(s, s->rotates[k].parent_xform, true))
+      return rt_set_error("bad rotate"), -1;
+  for (int k = 0; k < s->n_media; k++) {
+    const rt_medium &m = s->media[k];
+    const int bk = rt_ref_kind(m.boundary);
+    if (!ref_ok(s, m.boundary, false) || (bk != RT_KIND_SPHERE && bk != RT_KIND_QUAD) || m.phase_material < 0 ||
+        m.phase_material >= s->n_materials)
+      return rt_set_error("bad medium"), -1;
+  }
+  for (int k = 0; k < s->n_spheres; k++)
+    if (s->spheres[k].material < 0 || s->spheres[k].material >= s->n_materials) return rt_set_error("bad material"), -1;
+  for (int k = 0; k < s->n_quads; k++)
+    if (s->quads[k].material < 0 || s->quads[k].material >= s->n_materials) return rt_set_error("bad material"), -1;
+  for (int k = 0; k < s->n_materials; k++) {
+    const rt_material &m = s->materials[k];
+    const bool needs_tex = m.tag == RT_MAT_LAMBERTIAN || m.tag == RT_MAT_METAL || m.tag == RT_MAT_DIFFUSE_LIGHT ||
+                           m.tag == RT_MAT_ISOTROPIC;
+    if (m.tag < 0 || m.tag > RT_MAT_ISOTROPIC) return rt_set_error("bad material tag"), -1;
+    if (needs_tex && (m.texture < 0 || m.texture >= s->n_textures)) return rt_set_error("bad texture index"), -1;
+  }
+  for (int k = 0; k < s->n_textures; k++) {
+    const rt_texture &t = s->textures[k];
+    if (t.kind == RT_TEX_CHECKER && (t.a < 0 || t.a >= s->n_textures || t.b < 0 || t.b >= s->n_textures))
+      return rt_set_error("bad checker"), -1;
+    if (t.kind == RT_TEX_IMAGE) {
+      if (t.a < 0 || t.a >= s->n_images) return rt_set_error("bad image index"), -1;
+      const rt_image &im = s->images[t.a];
+      if (im.width <= 0 || im.height <= 0 || im.offset < 0 ||
+          im.offset + (int64_t)im.width * im.height * 3 > s->n_image_bytes)
+        return rt_set_error("bad image extent"), -1;
+    }
+    if (t.kind == RT_TEX_PERLIN) {
+      if (t.a < 0 || t.a >= s->n_perlins) return rt_set_error("bad perlin index"), -1;
+      const rt_perlin &p = s->perlins[t.a];
+      for (int q = 0; q < 256; q++)
+        if ((unsigned)p.perm_x[q] > 255 || (unsigned)p.perm_y[q] > 255 || (unsigned)p.perm_z[q] > 255)
+          return rt_set_error("bad perlin permutation"), -1;
+    }
+    if (t.kind < RT_TEX_SOLID || t.kind > RT_TEX_PERLIN) return rt_set_error("bad texture kind"), -1;
+  }
+  return 0;
+}
+
+extern "C" int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) {
+  if (s == NULL) {
+    rt_set_error("rt_scene_upload: NULL scene");
+    return NULL;
+  }
+  if (validate(s) != 0) return NULL;
+  if (hipSetDevice(device) != hipSuccess) {
+    rt_set_error("hipSetDevice(%d) failed", device);
+    return NULL;
+  }
+  struct Part {
+    const void *src;
+    size_t bytes;
+    size_t off;
+  };
+  Part parts[13] = {
+      {s->bvh, sizeof(rt_bvh_node) * s->n_bvh, 0},       {s->spheres, sizeof(rt_sphere) * s->n_spheres, 0},
+      {s->quads, sizeof(rt_quad) * s->n_quads, 0},       {s->lists, sizeof(rt_list) * s->n_lists, 0},
+      {s->list_items, sizeof(int32_t) * s->n_list_items, 0},
+      {s->translates, sizeof(rt_translate) * s->n_translates, 0},
+      {s->rotates, sizeof(rt_rotate_y) * s->n_rotates, 0}, {s->media, sizeof(rt_medium) * s->n_media, 0},
+      {s->materials, sizeof(rt_material) * s->n_materials, 0},
+      {s->textures, sizeof(rt_texture) * s->n_textures, 0}, {s->images, sizeof(rt_image) * s->n_images, 0},
+      {s->perlins, sizeof(rt_perlin) * s->n_perlins, 0},   {s->image_bytes, (size_t)s->n_image_bytes, 0}};
+  size_t total = 0;
+  for (auto &p : parts) {
+    p.off = total;
+    total = align_up(total + p.bytes, 256);
+  }
+  total = total ? total : 256;
+  void *arena = NULL;
+  if (hipMalloc(&arena, total) != hipSuccess) {
+    rt_set_error("hipMalloc(%zu) failed on device %d", total, device);
+    return NULL;
+  }
+  for (auto &p : parts)
+    if (p.bytes && hipMemcpy((char *)arena + p.off, p.src, p.bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(arena);
+      rt_set_error("scene upload failed on device %d", device);
+      return NULL;
+    }
+  rt_device_scene *d = new rt_device_scene();
+  d->device = device;
+  d->arena = arena;
+  d->arena_bytes = total;
+  d->features = s->features;
+  d->width = s->camera.width;
+  d->height = s->camera.height;
+  DScene &v = d->view;
+  memset(&v, 0, sizeof v);
+  v.cam = s->camera;
+  v.root = s->root;
+  v.lights = s->lights;
+  v.features = s->features;
+  char *b = (char *)arena;
+  v.bvh = (const rt_bvh_node *)(b + parts[0].off);
+  v.spheres = (const rt_sphere *)(b + parts[1].off);
+  v.quads = (const rt_quad *)(b + parts[2].off);
+  v.lists = (const rt_list *)(b + parts[3].off);
+  v.items = (const int32_t *)(b + parts[4].off);
+  v.translates = (const rt_translate *)(b + parts[5].off);
+  v.rotates = (const rt_rotate_y *)(b + parts[6].off);
+  v.media = (const rt_medium *)(b + parts[7].off);
+  v.materials = (const rt_material *)(b + parts[8].off);
+  v.textures = (const rt_texture *)(b + parts[9].off);
+  v.images = (const rt_image *)(b + parts[10].off);
+  v.perlins = (const rt_perlin *)(b + parts[11].off);
+  v.image_bytes = (const uint8_t *)(b + parts[12].off);
+  v.n_textures = s->n_textures;
+  v.n_images = s->n_images;
+  return d;
+}
+
+extern "C" void rt_scene_release(rt_device_scene *d) {
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  (void)hipFree(d->arena);
+  delete d;
+}
+
+extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out,
+                                    void *stream) {
+  if (!d || !d_out) return rt_set_error("rt_render_rows_async: NULL argument"), -1;
+  if (n_rows <= 0) return 0;
+  if (row0 < 0 || row_stride <= 0 || (int64_t)row0 + (int64_t)(n_rows - 1) * row_stride >= d->height)
+    return rt_set_error("rows %d + k*%d (k < %d) outside image height %d", row0, row_stride, n_rows, d->height), -1;
+  HIP_OK(hipSetDevice(d->device));
+  const int64_t npix = (int64_t)n_rows * d->width;
+  const dim3 grid((unsigned)((npix + kBlock - 1) / kBlock)), block(kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if ((d->features & ~kFeatBook1) == 0)
+    hipLaunchKernelGGL(rt_render_rows_kernel<kFeatBook1>, grid, block, 0, st, d->view, row0, row_stride, n_rows, d_out);
+  else
+    hipLaunchKernelGGL(rt_render_rows_kernel<kFeatAll>, grid, block, 0, st, d->view, row0, row_stride, n_rows, d_out);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ whole frame
+static std::mutex g_timing_mu;
+static std::vector<double> g_kernel_ms(64, 0.0);
+
+extern "C" double rt_last_kernel_ms(int device) {
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  return (device >= 0 && device < (int)g_kernel_ms.size()) ? g_kernel_ms[device] : 0.0;
+}
+
+extern "C" int rt_render(const rt_flat_scene *s, int n_gpus, uint8_t *out_host) {
+  if (!s || !out_host) return rt_set_error("rt_render: NULL argument"), -1;
+  const int avail = rt_device_count();
+  if (avail <= 0) return rt_set_error("rt_render: no HIP device visible (this library has no CPU path)"), -1;
+  const int H = s->camera.height, W = s->camera.width;
+  int G = (n_gpus <= 0 || n_gpus > avail) ? avail : n_gpus;
+  if (G > H) G = H;
+  struct PerGpu {
+    rt_device_scene *scene = nullptr;
+    uint8_t *d_out = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    int n_rows = 0;
+  };
+  std::vector<PerGpu> per(G);
+  int rc = 0;
+  for (int g = 0; g < G && rc == 0; g++) {  // upload + launch on every GPU first
+    PerGpu &p = per[g];
+    p.n_rows = (H - g + G - 1) / G;
+    p.scene = rt_scene_upload(s, g);
+    if (!p.scene) {
+      rc = -1;
+      break;
+    }
+    if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&p.d_out, (size_t)p.n_rows * W * 3) != hipSuccess || hipEventCreate(&p.t0) != hipSuccess ||
+        hipEventCreate(&p.t1) != hipSuccess) {
+      rt_set_error("rt_render: stream/buffer setup failed on device %d", g);
+      rc = -1;
+      break;
+    }
+    (void)hipEventRecord(p.t0, p.stream);
+    if (rt_render_rows_async(p.scene, g, G, p.n_rows, p.d_out, p.stream) != 0) {
+      rc = -1;
+      break;
+    }
+    (void)hipEventRecord(p.t1, p.stream);
+  }
+  std::vector<uint8_t> rows;
+  for (int g = 0; g < G; g++) {  // then drain: D2H compact rows, scatter to j % G == g
+    PerGpu &p = per[g];
+    if (rc == 0 && p.scene) {
+      (void)hipSetDevice(g);
+      rows.resize((size_t)p.n_rows * W * 3);
+      hipError_t e = hipStreamSynchronize(p.stream);
+      if (e == hipSuccess) e = hipMemcpy(rows.data(), p.d_out, rows.size(), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        rt_set_error("rt_render: device %d: %s", g, hipGetErrorString(e));
+        rc = -1;
+      } else {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, p.t0, p.t1);
+        {
+          std::lock_guard<std::mutex> lk(g_timing_mu);
+          if (g < (int)g_kernel_ms.size()) g_kernel_ms[g] = ms;
+        }
+        for (int k = 0; k < p.n_rows; k++)
+          memcpy(out_host + (size_t)(g + k * G) * W * 3, rows.data() + (size_t)k * W * 3, (size_t)W * 3);
+      }
+    }
+    if (p.scene) (void)hipSetDevice(g);
+    if (p.t0) (void)hipEventDestroy(p.t0);
+    if (p.t1) (void)hipEventDestroy(p.t1);
+    if (p.d_out) (void)hipFree(p.d_out);
+    if (p.stream) (void)hipStreamDestroy(p.stream);
+    rt_scene_release(p.scene);
+  }
+  return rc;
+}
+
+extern "C" int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device) {
+  if (n <= 0) return 0;
+  HIP_OK(hipSetDevice(device));
+  const int64_t nout = (fn == 0) ? 2 * n : n;
+  float *dx = NULL, *dy = NULL;
+  HIP_OK(hipMalloc(&dx, n * sizeof(float)));
+  HIP_OK(hipMalloc(&dy, nout * sizeof(float)));
+  HIP_OK(hipMemcpy(dx, x_host, n * sizeof(float), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(rt_diag_libm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, dx, dy, n);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpy(out_host, dy, nout * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_OK(hipFree(dx));
+  HIP_OK(hipFree(dy));
+  return 0;
+}

@@ -1,0 +1,307 @@
+// rt_libm.h — bit-exact restatement of the glibc 2.35 (x86-64, FMA ifunc) single-precision
+// transcendentals that sit on the reference's hot path, compiled for BOTH gfx950 device code and
+// the host (hipcc host pass) so one source can be checked exhaustively against the host glibc.
+//
+// Why: the reference (C11, gcc) calls libm inside the per-sample loop and a single differing bit
+// in a decision value desyncs a pixel's sequential pcg32 stream.  glibc is not
+// correctly rounded on these domains, so the GPU must reproduce glibc's algorithm, not the math.
+//
+// Call sites in the reference (ray-tracing-c @ v2):
+//   sincosf  src/material.c:26-27 (rand_cosine_theta; gcc merges cosf+sinf into sincosf),
+//            src/hittable.c:171-173 (Sphere_rand)
+//   powf     src/material.c:73      (Dielectric Schlick term, y = 5)
+//   logf     src/hittable.c:413     (ConstantMedium free-flight distance)
+//   sinf     src/texture.c:50       (Perlin marble)
+//
+// Algorithm + tables: glibc sysdeps/ieee754/flt-32/{s_sincosf.c,sincosf.h,e_powf.c,e_logf.c,
+// s_sinf.c} (ARM optimized-routines).  The FMA placement below is the one gcc emitted for the
+// `*_fma` ifunc variants that glibc selects on FMA-capable x86-64 (read off the disassembly of
+// /lib/x86_64-linux-gnu/libm.so.6, glibc 2.35-0ubuntu3.11); the table words were read from the
+// same library (oracle/tools/extract_libm_tables.c).  tests/test_libm_port.py checks every port
+// against the host libm over the full domain the hot path can feed it.
+//
+// Compile with -ffp-contract=off: every fused multiply-add below is an explicit fma().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RT_HD __host__ __device__ __forceinline__
+
+namespace rtm {
+
+RT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+RT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+RT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
+RT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
+RT_HD double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// ---------------------------------------------------------------- sincosf / sinf
+// sincos_t layout: sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4  (14 doubles, 2 copies).
+struct SinCosTab {
+  double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
+};
+
+RT_HD const SinCosTab &sincos_tab(int which) {
+  static constexpr SinCosTab T[2] = {
+      {{0x1p+0, -0x1p+0, -0x1p+0, 0x1p+0},
+       0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+       0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+       0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+      {{0x1p+0, -0x1p+0, -0x1p+0, 0x1p+0},
+       0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+       -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+       0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
+  };
+  return T[which];
+}
+
+// __inv_pio4: 4/pi bits, used by the |x| >= 120 reduction.
+RT_HD uint32_t inv_pio4(int i) {
+  static constexpr uint32_t T[24] = {
+      0x000000a2, 0x0000a2f9, 0x00a2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+      0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+      0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
+  return T[i];
+}
+
+RT_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ff; }
+
+// sincosf_poly with the FMA contraction of __sincosf_fma: returns (sin, cos) of the reduced
+// argument, already swapped for odd quadrants.
+RT_HD void sincos_poly(double x, double x2, const SinCosTab &p, int n, float *sinp, float *cosp) {
+  double x3 = x2 * x;
+  double x4 = x2 * x2;
+  double s1 = fmad(x2, p.s3, p.s2);
+  double c2 = fmad(x2, p.c4, p.c3);
+  double c1 = fmad(x2, p.c1, p.c0);
+  double x5 = x3 * x2;
+  double x6 = x4 * x2;
+  double s = fmad(x3, p.s1, x);
+  double c = fmad(x4, p.c2, c1);
+  float sv = (float)fmad(s1, x5, s);
+  float cv = (float)fmad(c2, x6, c);
+  if (n & 1) { *sinp = cv; *cosp = sv; }
+  else { *sinp = sv; *cosp = cv; }
+}
+
+// reduce_fast: x - n*pi/2 with n = round(x*2/pi) via the 2^24-scaled integer trick; the
+// subtraction is one fused negative multiply-add in the FMA build.
+RT_HD double reduce_fast(double x, const SinCosTab &p, int *np) {
+  double r = x * p.hpi_inv;
+  int n = ((int32_t)r + 0x800000) >> 24;
+  *np = n;
+  return fmad(-(double)n, p.hpi, x);
+}
+
+RT_HD double reduce_large(uint32_t xi, int *np) {
+  const int base = (xi >> 26) & 15;
+  const int shift = (xi >> 23) & 7;
+  xi = (xi & 0xffffff) | 0x800000;
+  xi <<= shift;
+  uint64_t res0 = (uint32_t)(xi * inv_pio4(base + 0));
+  uint64_t res1 = (uint64_t)xi * inv_pio4(base + 4);
+  uint64_t res2 = (uint64_t)xi * inv_pio4(base + 8);
+  res0 = (res2 >> 32) | (res0 << 32);
+  res0 += res1;
+  uint64_t n = (res0 + (1ULL << 61)) >> 62;
+  res0 -= n << 62;
+  double x = (double)(int64_t)res0;
+  *np = (int)n;
+  return x * 0x1.921fb54442d18p-62;
+}
+
+// glibc sincosf (finite inputs; NaN/inf return NaN like glibc, without errno).
+RT_HD void sincosf(float y, float *sinp, float *cosp) {
+  double x = y;
+  int n;
+  const uint32_t at = abstop12(y);
+  if (at < 0x3f4) {                       // |y| < pi/4
+    double x2 = x * x;
+    if (at < 0x398) {                     // |y| < 2^-12
+      *sinp = y;
+      *cosp = 1.0f;
+      return;
+    }
+    sincos_poly(x, x2, sincos_tab(0), 0, sinp, cosp);
+  } else if (at < 0x42f) {                // |y| < 120
+    x = reduce_fast(x, sincos_tab(0), &n);
+    const double s = sincos_tab(0).sign[n & 3];
+    const SinCosTab &p = sincos_tab((n & 2) ? 1 : 0);
+    sincos_poly(x * s, x * x, p, n, sinp, cosp);
+  } else if (at < 0x7f8) {                // finite
+    const uint32_t xi = f2u(y);
+    const int sign = xi >> 31;
+    x = reduce_large(xi, &n);
+    const double s = sincos_tab(0).sign[(n + sign) & 3];
+    const SinCosTab &p = sincos_tab(((n + sign) & 2) ? 1 : 0);
+    sincos_poly(x * s, x * x, p, n, sinp, cosp);
+  } else {
+    *sinp = *cosp = y - y;
+  }
+}
+
+// glibc sinf: the same reduction and the sin/cos halves of the same polynomial.
+RT_HD float sinf(float y) {
+  float s, c;
+  sincosf(y, &s, &c);
+  return s;
+}
+
+// ---------------------------------------------------------------- powf
+RT_HD double powf_log2_invc(int i) {
+  static constexpr double T[16] = {
+      0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0, 0x1.3c995b0b80385p+0,
+      0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+      0x1.0953f419900a7p+0, 0x1p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+      0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+  return T[i];
+}
+RT_HD double powf_log2_logc(int i) {
+  static constexpr double T[16] = {
+      -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+      -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3, -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
+      -0x1.a6f9db6475fcep-5, 0x0p+0, 0x1.338ca9f24f53dp-4, 0x1.476a9543891bap-3,
+      0x1.e840b4ac4e4d2p-3, 0x1.40645f0c6651cp-2, 0x1.88e9c2c1b9ff8p-2, 0x1.ce0a44eb17bccp-2};
+  return T[i];
+}
+RT_HD uint64_t exp2f_tab(int i) {
+  static constexpr uint64_t T[32] = {
+      0x3ff0000000000000, 0x3fefd9b0d3158574, 0x3fefb5586cf9890f, 0x3fef9301d0125b51,
+      0x3fef72b83c7d517b, 0x3fef54873168b9aa, 0x3fef387a6e756238, 0x3fef1e9df51fdee1,
+      0x3fef06fe0a31b715, 0x3feef1a7373aa9cb, 0x3feedea64c123422, 0x3feece086061892d,
+      0x3feebfdad5362a27, 0x3feeb42b569d4f82, 0x3feeab07dd485429, 0x3feea47eb03a5585,
+      0x3feea09e667f3bcd, 0x3fee9f75e8ec5f74, 0x3feea11473eb0187, 0x3feea589994cce13,
+      0x3feeace5422aa0db, 0x3feeb737b0cdc5e5, 0x3feec49182a3f090, 0x3feed503b23e255d,
+      0x3feee89f995ad3ad, 0x3feeff76f2fb5e47, 0x3fef199bdd85529c, 0x3fef3720dcef9069,
+      0x3fef5818dcfba487, 0x3fef7c97337b9b5f, 0x3fefa4afa2a490da, 0x3fefd0765b6e4540};
+  return T[i];
+}
+
+RT_HD bool zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000 - 1; }
+
+// checkint: 0 = not an integer, 1 = odd integer, 2 = even integer.
+RT_HD int checkint(uint32_t iy) {
+  int e = (iy >> 23) & 0xff;
+  if (e < 0x7f) return 0;
+  if (e > 0x7f + 23) return 2;
+  if (iy & ((1u << (0x7f + 23 - e)) - 1)) return 0;
+  if (iy & (1u << (0x7f + 23 - e))) return 1;
+  return 2;
+}
+
+RT_HD double powf_log2_inline(uint32_t ix) {
+  const uint32_t tmp = ix - 0x3f330000;
+  const int i = (tmp >> 19) % 16;
+  const uint32_t top = tmp & 0xff800000;
+  const uint32_t iz = ix - top;
+  const int k = (int32_t)top >> 23;
+  const double invc = powf_log2_invc(i), logc = powf_log2_logc(i);
+  const double z = (double)u2f(iz);
+  const double r = fmad(z, invc, -1.0);
+  const double y0 = (double)k + logc;
+  const double r2 = r * r;
+  double y = fmad(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
+  const double p = fmad(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+  const double r4 = r2 * r2;
+  double q = fmad(0x1.71547652ab82bp+0, r, y0);
+  q = fmad(p, r2, q);
+  y = fmad(y, r4, q);
+  return y;
+}
+
+RT_HD double powf_exp2_inline(double xd, uint32_t sign_bias) {
+  const double shift = 0x1.8p+47;
+  double kd = xd + shift;
+  const uint64_t ki = d2u(kd);
+  kd -= shift;
+  const double r = xd - kd;
+  uint64_t t = exp2f_tab((int)(ki % 32));
+  const uint64_t ski = ki + sign_bias;
+  t += ski << (52 - 5);
+  const double s = u2d(t);
+  const double z = fmad(0x1.c6af84b912394p-5, r, 0x1.ebfce50fac4f3p-3);
+  const double r2 = r * r;
+  double y = fmad(0x1.62e42ff0c52d6p-1, r, 1.0);
+  y = fmad(z, r2, y);
+  return y * s;
+}
+
+// glibc powf (round-to-nearest, errno-free).
+RT_HD float powf(float x, float y) {
+  uint32_t sign_bias = 0;
+  uint32_t ix = f2u(x), iy = f2u(y);
+  if (ix - 0x00800000 >= 0x7f800000 - 0x00800000 || zeroinfnan(iy)) {
+    if (zeroinfnan(iy)) {
+      if (2 * iy == 0) return 1.0f;
+      if (ix == 0x3f800000) return 1.0f;
+      if (2 * ix > 2u * 0x7f800000 || 2 * iy > 2u * 0x7f800000) return x + y;
+      if (2 * ix == 2 * 0x3f800000) return 1.0f;
+      if ((2 * ix < 2 * 0x3f800000) == !(iy & 0x80000000)) return 0.0f;
+      return y * y;
+    }
+    if (zeroinfnan(ix)) {
+      float x2 = x * x;
+      if ((ix & 0x80000000) && checkint(iy) == 1) x2 = -x2;
+      return (iy & 0x80000000) ? 1.0f / x2 : x2;
+    }
+    if (ix & 0x80000000) {
+      const int yint = checkint(iy);
+      if (yint == 0) return (x - x) / (x - x);
+      if (yint == 1) sign_bias = 1u << (5 + 11);
+      ix &= 0x7fffffff;
+    }
+    if (ix < 0x00800000) {
+      ix = f2u(x * 0x1p23f);
+      ix &= 0x7fffffff;
+      ix -= 23u << 23;
+    }
+  }
+  const double logx = powf_log2_inline(ix);
+  const double ylogx = (double)y * logx;
+  if (((d2u(ylogx) >> 47) & 0xffff) >= (d2u(126.0) >> 47)) {
+    const float sgn = sign_bias ? -1.0f : 1.0f;
+    if (ylogx > 0x1.fffffffd1d571p+6) return sgn * 0x1p97f * 0x1p97f;           // overflow
+    // (0x1.fffffffa3aae2p+6 < ylogx only overflows in directed rounding modes: falls through.)
+    if (ylogx <= -150.0) return sgn * 0x1p-95f * 0x1p-95f;                      // underflow
+    if (ylogx < -149.0) return sgn * 0x1.4p-75f * 0x1.4p-75f;                   // may underflow
+  }
+  return (float)powf_exp2_inline(ylogx, sign_bias);
+}
+
+// ---------------------------------------------------------------- logf
+RT_HD double logf_logc(int i) {
+  static constexpr double T[16] = {
+      -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
+      -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3, -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4,
+      -0x1.252f438e10c1ep-5, 0x0p+0, 0x1.aa5aa5df25984p-5, 0x1.c5e53aa362eb4p-4,
+      0x1.526e57720db08p-3, 0x1.bc2860d22477p-3, 0x1.1058bc8a07ee1p-2, 0x1.4043057b6ee09p-2};
+  return T[i];
+}
+
+// glibc logf (round-to-nearest, errno-free).
+RT_HD float logf(float x) {
+  uint32_t ix = f2u(x);
+  if (ix == 0x3f800000) return 0.0f;
+  if (ix - 0x00800000 >= 0x7f800000 - 0x00800000) {
+    if (ix * 2 == 0) return -__builtin_inff();
+    if (ix == 0x7f800000) return x;
+    if ((ix & 0x80000000) || ix * 2 >= 0xff000000) return (x - x) / (x - x);
+    ix = f2u(x * 0x1p23f);
+    ix -= 23u << 23;
+  }
+  const uint32_t tmp = ix - 0x3f330000;
+  const int i = (tmp >> 19) % 16;
+  const int k = (int32_t)tmp >> 23;
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  const double invc = powf_log2_invc(i), logc = logf_logc(i);
+  const double z = (double)u2f(iz);
+  const double r = fmad(z, invc, -1.0);
+  const double y0 = fmad((double)k, 0x1.62e42fefa39efp-1, logc);
+  const double r2 = r * r;
+  double y = fmad(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
+  y = fmad(-0x1.00ea348b88334p-2, r2, y);
+  y = fmad(y, r2, y0 + r);
+  return (float)y;
+}
+
+}  // namespace rtm

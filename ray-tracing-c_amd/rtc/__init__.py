@@ -1,0 +1,226 @@
+"""rtc — Python view of the MI355X render path (ctypes over the C ABI in include/rt_hip.h).
+
+The product is the C library ``ray-tracing-c_amd/librtc_amd.so`` (drop-in ``Camera_render`` + the
+gfx950 kernels).  This module only binds it for tests and ``bench.py``; it adds no compute of its
+own and has no fallback: if the library or a GPU is missing, calls raise ``RtcError``.
+
+Reference boundary mirrored: ``void Camera_render(const Camera*, const World*, uint8_t*)``
+(reference include/raytracing.h:41, src/raytracing.c:86-135).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # ray-tracing-c_amd/
+LIB_PATH = os.path.join(PKG_DIR, "librtc_amd.so")
+
+# rt_feature_bits (include/rt_flat.h)
+FEAT_BVH, FEAT_QUAD, FEAT_XFORM, FEAT_MEDIUM = 1, 2, 4, 8
+FEAT_LIGHTS, FEAT_TEX_UV, FEAT_TEX_PERLIN, FEAT_EMISSIVE, FEAT_DOF = 16, 32, 64, 128, 256
+
+# reference scene ids (src/main.c:294-329) and their names
+SCENES = {
+    0: "Book 1: Metal and Lambertian",
+    1: "Book 1: Final scene",
+    2: "Book 2: Checker",
+    3: "Book 2: Earth",
+    4: "Book 2: Perlin noise",
+    5: "Book 2: Simple light",
+    6: "Book 2: Cornell box",
+    7: "Book 2: Final scene",
+}
+
+
+class RtcError(RuntimeError):
+    pass
+
+
+class RtCamera(ctypes.Structure):
+    _fields_ = [
+        ("width", c_int32), ("height", c_int32), ("spp", c_int32), ("max_depth", c_int32),
+        ("pixel00", c_float * 3), ("dof_angle", c_float),
+        ("delta_u", c_float * 3), ("light_prob", c_float),
+        ("delta_v", c_float * 3), ("pad0", c_float),
+        ("origin", c_float * 3), ("pad1", c_float),
+        ("disc_u", c_float * 3), ("pad2", c_float),
+        ("disc_v", c_float * 3), ("pad3", c_float),
+        ("background", c_float * 3), ("pad4", c_float),
+    ]
+
+
+_COUNTS = ["n_bvh", "n_spheres", "n_quads", "n_lists", "n_list_items", "n_translates", "n_rotates",
+           "n_media", "n_materials", "n_textures", "n_images", "n_perlins"]
+_ARRAYS = ["bvh", "spheres", "quads", "lists", "list_items", "translates", "rotates", "media",
+           "materials", "textures", "images", "perlins", "image_bytes"]
+
+
+class RtFlatScene(ctypes.Structure):
+    _fields_ = ([("camera", RtCamera), ("root", c_int32), ("lights", c_int32), ("features", c_int32),
+                 ("stack_needed", c_int32)]
+                + [(n, c_int32) for n in _COUNTS]
+                + [("n_image_bytes", c_int64)]
+                + [(n, c_void_p) for n in _ARRAYS])
+
+
+assert ctypes.sizeof(RtCamera) == 128
+assert RtFlatScene.n_image_bytes.offset == 192
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librtc_amd.so (built by ``make -C ray-tracing-c_amd``)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtcError(f"{LIB_PATH} not built: run `make -C ray-tracing-c_amd` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        P = POINTER(RtFlatScene)
+        L.rt_scene_preset.argtypes = [c_int, c_int, c_int, c_int]
+        L.rt_scene_preset.restype = P
+        L.rt_flat_free.argtypes = [P]
+        L.rt_flat_free.restype = None
+        L.rt_device_count.restype = c_int
+        L.rt_scene_upload.argtypes = [P, c_int]
+        L.rt_scene_upload.restype = c_void_p
+        L.rt_scene_release.argtypes = [c_void_p]
+        L.rt_scene_release.restype = None
+        L.rt_render_rows_async.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
+        L.rt_render_rows_async.restype = c_int
+        L.rt_render.argtypes = [P, c_int, c_void_p]
+        L.rt_render.restype = c_int
+        L.rt_last_kernel_ms.argtypes = [c_int]
+        L.rt_last_kernel_ms.restype = c_double
+        L.rt_diag_libm.argtypes = [c_int, c_void_p, c_void_p, c_int64, c_int]
+        L.rt_diag_libm.restype = c_int
+        L.rt_last_error.restype = c_char_p
+        L.rt_abi_version.restype = c_int
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().rt_last_error() or b"").decode(errors="replace")
+
+
+class Scene:
+    """An owned rt_flat_scene (host memory)."""
+
+    def __init__(self, ptr):
+        if not ptr:
+            raise RtcError(f"scene construction failed: {last_error()}")
+        self._ptr = ptr
+
+    @classmethod
+    def preset(cls, scene_id: int, width: int = 0, spp: int = 0, max_depth: int = 0) -> "Scene":
+        """Reference driver scene `scene_id` (0-7) with the reference defaults (500 px, 100 spp,
+        depth 50) unless overridden; aspect ratio comes from the scene (src/main.c)."""
+        return cls(lib().rt_scene_preset(int(scene_id), int(width), int(spp), int(max_depth)))
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    @property
+    def s(self) -> RtFlatScene:
+        return self._ptr.contents
+
+    @property
+    def width(self) -> int:
+        return self.s.camera.width
+
+    @property
+    def height(self) -> int:
+        return self.s.camera.height
+
+    @property
+    def spp(self) -> int:
+        return self.s.camera.spp
+
+    @property
+    def max_depth(self) -> int:
+        return self.s.camera.max_depth
+
+    @property
+    def features(self) -> int:
+        return self.s.features
+
+    def counts(self) -> dict:
+        return {n: getattr(self.s, n) for n in _COUNTS + ["stack_needed"]}
+
+    def close(self):
+        if self._ptr:
+            lib().rt_flat_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    return lib().rt_device_count()
+
+
+def render(scene: Scene, n_gpus: int = 1) -> np.ndarray:
+    """Whole frame on the GPU(s) into a host (H, W, 3) uint8 array (what Camera_render does)."""
+    out = np.empty((scene.height, scene.width, 3), dtype=np.uint8)
+    rc = lib().rt_render(scene.ptr, int(n_gpus), out.ctypes.data)
+    if rc != 0:
+        raise RtcError(f"rt_render failed: {last_error()}")
+    return out
+
+
+def last_kernel_ms(device: int = 0) -> float:
+    return lib().rt_last_kernel_ms(device)
+
+
+class DeviceScene:
+    """Scene arrays resident in one GPU's HBM (rt_scene_upload)."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        self.scene = scene
+        self.device = device
+        self._h = lib().rt_scene_upload(scene.ptr, int(device))
+        if not self._h:
+            raise RtcError(f"rt_scene_upload failed: {last_error()}")
+
+    def render_rows_async(self, row0: int, row_stride: int, n_rows: int, d_out_ptr: int, stream_ptr: int = 0):
+        rc = lib().rt_render_rows_async(self._h, int(row0), int(row_stride), int(n_rows),
+                                        c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
+        if rc != 0:
+            raise RtcError(f"rt_render_rows_async failed: {last_error()}")
+
+    def close(self):
+        if self._h:
+            lib().rt_scene_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rows_of(height: int, rank: int, world: int):
+    """Interleaved row partition j % world == rank: (row0, stride, n_rows)."""
+    n = (height - rank + world - 1) // world if rank < height else 0
+    return rank, world, max(n, 0)
+
+
+def diag_libm(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:
+    """Evaluate the device libm port (0 sincosf, 1 powf(x,5), 2 logf, 3 sinf) on float32 inputs."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(2 * x.size if fn == 0 else x.size, dtype=np.float32)
+    rc = lib().rt_diag_libm(int(fn), x.ctypes.data, out.ctypes.data, x.size, int(device))
+    if rc != 0:
+        raise RtcError(f"rt_diag_libm failed: {last_error()}")
+    return out
