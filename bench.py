@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the MI355X render path on the reference's headline benchmark.
+
+Workload (BASELINE.json configs[2]): the Book-1 final scene (reference CLI scene 1, src/main.c:32-85),
+1200x675, 1000 samples per pixel, max depth 50 — exactly `./main 1 1200 1000 _` of the reference.
+A "step" is one full frame: every pixel's 1000-sample path loop, i.e. one kernel launch per GPU
+over that GPU's rows.  The scene arrays are resident in HBM before timing starts; the frame stays
+in HBM (the PCIe-inclusive end-to-end rate of Camera_render is reported separately in DESIGN.md).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, rows j % N == rank, no collective on the data path; the frame is fixed, so this
+is strong scaling.  Timing: barrier + synchronize on both sides of K steps, max over ranks.
+
+After timing (outside the timed region) the ranks' rows are gathered and the frame's sha256 is
+compared with the reference render's (tests/golden/manifest.json) when that config has a golden.
+
+rank 0 at N=1 first times the reference's own CPU build (oracle/_ref/ref_render_fast: upstream
+`-std=c11 -Ofast -fopenmp`) on a bounded sample of the same workload, before the GPU is touched.
+"""
+import argparse
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ray-tracing-c_amd"))
+
+METRIC = "Msamples/s (pixels×spp) Book-1 final 1200×675×1000spp; max-abs pixel diff"
+# FP32 operations per sample (instrumented reference event counts x per-event op counts)
+OPS_PER_SAMPLE = {0: 0.48e3, 1: 2.82e3, 7: 6.0e3}
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+README_M1_MSAMPLES = 5.26     # README.md:43, 2 min 34 s on a MacBook Air M1 (derived)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--cpu-spp", type=int, default=100, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Reference CPU build (upstream flags) on a bounded sample: same scene and size, fewer spp."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle  # test infrastructure: used only as the measured CPU baseline here
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    kind, exe = "reference", pyoracle.REF_FAST
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        t0 = time.perf_counter()
+        w, h = pyoracle.ref_render(args.scene, args.width, args.cpu_spp, args.depth, os.path.join(td, "o.rgb"),
+                                   fast=True, threads=threads, timeout=600)
+        dt = time.perf_counter() - t0
+    return {"value": round(w * h * args.cpu_spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": kind,
+            "sample": (f"scene {args.scene} {w}x{h} at {args.cpu_spp} spp (of {args.spp}), depth {args.depth}: the "
+                       f"reference sources built with its Makefile flags -std=c11 -Ofast -fopenmp "
+                       f"(oracle/_ref/ref_render_fast), {threads} OpenMP threads, wall {dt:.2f} s"),
+            "host_cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def golden_for(args):
+    try:
+        man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))
+    except OSError:
+        return None, None
+    for name, e in man.get("renders", {}).items():
+        if (e["scene"], e["width"], e["spp"], e["depth"]) == (args.scene, args.width, args.spp, args.depth):
+            return name, e
+    return None, None
+
+
+def traffic_for(config_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_traffic.json)."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        return t.get(config_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(args)  # before anything initialises the GPU
+
+    import torch
+    import torch.distributed as dist
+
+    import rtc
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    sc = rtc.Scene.preset(args.scene, args.width, args.spp, args.depth)
+    W, H, spp = sc.width, sc.height, sc.spp
+    row0, stride, n_rows = rtc.rows_of(H, rank, world)
+    ds = rtc.DeviceScene(sc, local)
+    buf = torch.zeros((max(n_rows, 1), W, 3), dtype=torch.uint8, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream(local)
+
+    def step():
+        if n_rows > 0:
+            ds.render_rows_async(row0, stride, n_rows, buf.data_ptr(), stream.cuda_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        step()
+        ends[k].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / max(args.steps, 1)
+
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms_max = t.tolist()
+    else:
+        kernel_ms_max = kernel_ms
+
+    # ---- parity (outside the timed region): gather rows, compare the frame with the reference
+    parity = None
+    if not args.no_parity:
+        rows = buf[:n_rows]
+        if world > 1:
+            m = (H + world - 1) // world
+            pad = torch.zeros((m, W, 3), dtype=torch.uint8, device=buf.device)
+            pad[:n_rows] = rows
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad)
+        else:
+            parts = [rows]
+        if rank == 0:
+            frame = torch.empty((H, W, 3), dtype=torch.uint8)
+            for r, p in enumerate(parts):
+                r0, st, n = rtc.rows_of(H, r, world)
+                frame[r0::st][:n] = p[:n].cpu()
+            sha = hashlib.sha256(frame.numpy().tobytes()).hexdigest()
+            name, g = golden_for(args)
+            parity = {"frame_sha256": sha, "golden": name,
+                      "pixel_identical_to_reference": (sha == g["sha256"]) if g else None,
+                      "max_abs_pixel_diff": 0 if (g and sha == g["sha256"]) else None}
+
+    if rank == 0:
+        frame_samples = W * H * spp
+        value = frame_samples * args.steps / elapsed / 1e6
+        ops = OPS_PER_SAMPLE.get(args.scene)
+        launch_samples = n_rows * W * spp
+        achieved = (launch_samples * ops / (kernel_ms / 1e3) / 1e12) if ops else None
+        workload = (f"Book-1 final scene (reference CLI scene 1) {W}x{H}, {spp} spp, depth {args.depth}"
+                    if args.scene == 1 else f"reference scene {args.scene} {W}x{H}, {spp} spp, depth {args.depth}")
+        config_key = f"s{args.scene}_{W}x{H}_{spp}spp_d{args.depth}_n{world}"
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / README_M1_MSAMPLES, 2) if (args.scene == 1 and W == 1200 and spp == 1000
+                                                                    and args.depth == 50) else None,
+            "vs_baseline_source": "README.md:43 (2 min 34 s, M1, OpenMP) => 5.26 Msamples/s, BASELINE.md",
+            "dtype": "f32",
+            "data": "synthetic: the reference's procedural scene (pcg32 seed 19,29) and per-pixel pcg32 streams",
+            "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
+                       "max_depth": args.depth, "partition": f"rows j % {world}", "rows_on_rank0": n_rows},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 4) if achieved else None,
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 5) if achieved else None,
+                         "traffic": traffic_for(config_key),
+                         "kernel": "rt_render_rows_kernel", "kernel_ms_avg": round(kernel_ms, 3),
+                         "kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
+                         "algorithmic_work": f"{ops:.0f} FP32 ops/sample (SURVEY §8d) x {launch_samples} samples/launch"
+                         if ops else None,
+                         "note": "branchy FP32 VALU + u64 integer work, no MFMA; scene is L1/L2 resident, so the "
+                                 "HBM roof does not apply; peak = FP32 vector (= f32 MFMA) rate"},
+            "cpu_baseline": base,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+
+    ds.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -486,3 +486,109 @@ int oracle_render_pixels(const rt_flat_scene *S, const int32_t *xs, const int32_
   for (int k = 0; k < n; k++) pixel(S, xs[k], ys[k], out + 3 * (long)k);
   return 0;
 }
+
+/* ------------------------------------------------------------------ canonical dump
+ * Same text format as oracle/ref_harness.c `dump`, produced from the flattened scene, so a test
+ * can diff the scene this library builds against the scene the reference builds. */
+#include <stdio.h>
+static void dump_tex(FILE *f, const rt_flat_scene *S, int32_t id) {
+  if (id < 0) { fprintf(f, " tex=none"); return; }
+  const rt_texture *t = &S->textures[id];
+  if (t->kind == RT_TEX_SOLID) fprintf(f, " solid(%a %a %a)", t->color[0], t->color[1], t->color[2]);
+  else if (t->kind == RT_TEX_CHECKER) { fprintf(f, " checker(%a", t->scale); dump_tex(f, S, t->a); dump_tex(f, S, t->b); fprintf(f, ")"); }
+  else if (t->kind == RT_TEX_IMAGE) {
+    const rt_image *im = &S->images[t->a];
+    unsigned long long h = 1469598103934665603ULL;
+    for (long i = 0; i < (long)im->width * im->height * 3; i++) h = (h ^ S->image_bytes[im->offset + i]) * 1099511628211ULL;
+    fprintf(f, " image(%d %d %016llx)", im->width, im->height, h);
+  } else {
+    const rt_perlin *P = &S->perlins[t->a];
+    unsigned long long h = 1469598103934665603ULL;
+    for (int i = 0; i < 256; i++) {
+      unsigned int vv[6];
+      memcpy(vv, P->grad[i], 12);
+      vv[3] = (unsigned)P->perm_x[i]; vv[4] = (unsigned)P->perm_y[i]; vv[5] = (unsigned)P->perm_z[i];
+      for (int k = 0; k < 6; k++) h = (h ^ vv[k]) * 1099511628211ULL;
+    }
+    fprintf(f, " perlin(%a %d %016llx)", t->scale, P->depth, h);
+  }
+}
+static void dump_mat(FILE *f, const rt_flat_scene *S, int32_t id) {
+  const rt_material *m = &S->materials[id];
+  fprintf(f, " mat(%d %a", m->tag, m->param);
+  if (m->tag != RT_MAT_DIELECTRIC && m->tag != RT_MAT_SURFACE_NORMAL) dump_tex(f, S, m->texture);
+  fprintf(f, ")");
+}
+static void dump_ref(FILE *f, const rt_flat_scene *S, int32_t ref, int depth) {
+  fprintf(f, "%*s", depth, "");
+  if (ref == RT_REF_NONE) { fprintf(f, "NONE\n"); return; }
+  const int32_t i = rt_ref_index(ref);
+  switch (rt_ref_kind(ref)) {
+  case RT_KIND_LIST: {
+    const rt_list *l = &S->lists[i];
+    fprintf(f, "LIST %d\n", l->count);
+    for (int k = 0; k < l->count; k++) dump_ref(f, S, S->list_items[l->first + k], depth + 1);
+    break;
+  }
+  case RT_KIND_BVH: {
+    const rt_bvh_node *n = &S->bvh[i];
+    int dup = n->right == RT_REF_NONE || n->right == n->left;
+    fprintf(f, "BVH %a %a %a %a %a %a%s\n", n->lo[0], n->lo[1], n->lo[2], n->hi[0], n->hi[1], n->hi[2], dup ? " dup" : "");
+    dump_ref(f, S, n->left, depth + 1);
+    if (!dup) dump_ref(f, S, n->right, depth + 1);
+    break;
+  }
+  case RT_KIND_SPHERE: {
+    const rt_sphere *s = &S->spheres[i];
+    fprintf(f, "SPHERE %a %a %a %a", s->center[0], s->center[1], s->center[2], s->radius);
+    dump_mat(f, S, s->material);
+    fprintf(f, "\n");
+    break;
+  }
+  case RT_KIND_QUAD: {
+    const rt_quad *q = &S->quads[i];
+    fprintf(f, "QUAD %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a", q->Q[0], q->Q[1], q->Q[2], q->u[0], q->u[1],
+            q->u[2], q->v[0], q->v[1], q->v[2], q->normal[0], q->normal[1], q->normal[2], q->D, q->w[0], q->w[1],
+            q->w[2], q->area);
+    dump_mat(f, S, q->material);
+    fprintf(f, "\n");
+    break;
+  }
+  case RT_KIND_TRANSLATE: {
+    const rt_translate *t = &S->translates[i];
+    fprintf(f, "TRANSLATE %a %a %a\n", t->offset[0], t->offset[1], t->offset[2]);
+    dump_ref(f, S, t->child, depth + 1);
+    break;
+  }
+  case RT_KIND_ROTATE_Y: {
+    const rt_rotate_y *r = &S->rotates[i];
+    fprintf(f, "ROTATE %a %a\n", r->sin_theta, r->cos_theta);
+    dump_ref(f, S, r->child, depth + 1);
+    break;
+  }
+  case RT_KIND_MEDIUM: {
+    const rt_medium *m = &S->media[i];
+    fprintf(f, "MEDIUM %a", m->neg_inv_density);
+    dump_mat(f, S, m->phase_material);
+    fprintf(f, "\n");
+    dump_ref(f, S, m->boundary, depth + 1);
+    break;
+  }
+  }
+}
+int oracle_dump_flat(const rt_flat_scene *S, const char *path) {
+  FILE *f = fopen(path, "w");
+  if (!f) return -1;
+  const rt_camera *c = &S->camera;
+  fprintf(f, "CAMERA %d %d %a %a %a | %a %a %a | %a %a %a | %a %a %a | %a %a %a | %a %a %a | %a %a %a %a\n", c->width,
+          c->height, c->pixel00[0], c->pixel00[1], c->pixel00[2], c->delta_u[0], c->delta_u[1], c->delta_u[2],
+          c->delta_v[0], c->delta_v[1], c->delta_v[2], c->origin[0], c->origin[1], c->origin[2], c->disc_u[0],
+          c->disc_u[1], c->disc_u[2], c->disc_v[0], c->disc_v[1], c->disc_v[2], c->background[0], c->background[1],
+          c->background[2], c->dof_angle);
+  dump_ref(f, S, S->root, 0);
+  const rt_list *L = &S->lists[S->lights];
+  fprintf(f, "LIGHTS %d\n", L->count);
+  for (int k = 0; k < L->count; k++) dump_ref(f, S, S->list_items[L->first + k], 1);
+  fclose(f);
+  return 0;
+}

@@ -31,6 +31,8 @@ def lib():
         L.oracle_render_pixels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                            ctypes.c_void_p]
         L.oracle_render_pixels.restype = ctypes.c_int
+        L.oracle_dump_flat.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.oracle_dump_flat.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -68,3 +70,11 @@ def ref_render(scene_id: int, width: int, spp: int, depth: int, out_path: str, f
 
 def ref_available() -> bool:
     return os.path.exists(REF_STRICT)
+
+
+def dump_flat(scene, path: str) -> str:
+    """Canonical text dump of an rtc.Scene (same format as `ref_render dump`)."""
+    if lib().oracle_dump_flat(ctypes.cast(scene.ptr, ctypes.c_void_p), path.encode()) != 0:
+        raise RuntimeError("oracle_dump_flat failed")
+    with open(path) as f:
+        return f.read()

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE build (oracle/_ref/ref_render).
+
+Run in the build container, where /root/reference exists and `make -C oracle` has built
+oracle/_ref/ (the reference's own sources, strict gcc -std=c11 -O2; see oracle/Makefile).
+
+Writes (all small, all data):
+  kat.txt                 pcg32 / vec3_rand known answers from the reference's src/pcg32.c, src/vec3.c
+  scene<N>.dump.gz        canonical dump of the scene graph the reference builds (ref_render dump N)
+  tiff_header.bin         the 168-byte header the reference's write_tiff emits for a 400x225 RGB image
+  render_<cfg>.rgb.gz     full reference renders for small configs (raw RGB rows, top to bottom)
+  manifest.json           every render: scene/size/spp/depth, sha256 of the full RGB buffer, crops
+
+Usage: python tests/golden/make_golden.py [--big]   (--big adds the 1200x675x1000spp frame, ~8 min)
+"""
+import argparse
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref", "ref_render")
+
+# (name, scene, width, spp, depth, keep_full_image)
+SMALL = [
+    ("s0_400x225_10spp_d10", 0, 400, 10, 10, True),     # BASELINE config 1 (CPU plumbing case)
+    ("s0_400x225_100spp_d50", 0, 400, 100, 50, True),   # BASELINE config 2 (correctness gate)
+    ("s1_300x168_16spp_d50", 1, 300, 16, 50, True),
+    ("s1_1200x675_10spp_d50", 1, 1200, 10, 50, False),
+    ("s2_200x112_8spp_d50", 2, 200, 8, 50, True),
+    ("s3_200x112_8spp_d50", 3, 200, 8, 50, True),
+    ("s4_200x112_8spp_d50", 4, 200, 8, 50, True),
+    ("s5_200x112_16spp_d50", 5, 200, 16, 50, True),
+    ("s6_200x200_16spp_d50", 6, 200, 16, 50, True),
+    ("s7_200x200_8spp_d50", 7, 200, 8, 50, True),
+    ("s7_400x400_16spp_d50", 7, 400, 16, 50, False),
+]
+BIG = [("s1_1200x675_1000spp_d50", 1, 1200, 1000, 50, False)]  # the north-star frame
+
+
+def crops(img, w, h, n=8, size=32):
+    """Deterministic crop positions spread over the frame; returns {"x,y": sha256}."""
+    out = {}
+    xs = [0, w // 2 - size // 2, w - size, w // 4, 3 * w // 4 - size, w // 3, 2 * w // 3, w // 8]
+    ys = [0, h // 2 - size // 2, h - size, 3 * h // 4 - size, h // 4, h // 3, 2 * h // 3, h - size]
+    for x, y in list(zip(xs, ys))[:n]:
+        x, y = max(0, min(x, w - size)), max(0, min(y, h - size))
+        rows = b"".join(img[((y + r) * w + x) * 3:((y + r) * w + x + size) * 3] for r in range(size))
+        out[f"{x},{y}"] = hashlib.sha256(rows).hexdigest()
+    return out
+
+
+def render(name, scene, width, spp, depth, keep, manifest):
+    with tempfile.TemporaryDirectory() as td:
+        raw = os.path.join(td, "out.rgb")
+        r = subprocess.run([REF, "render", str(scene), str(width), str(spp), str(depth), raw],
+                           capture_output=True, text=True, check=True)
+        w, h = map(int, r.stdout.split()[:2])
+        img = open(raw, "rb").read()
+    assert len(img) == w * h * 3
+    entry = {"scene": scene, "width": w, "height": h, "spp": spp, "depth": depth,
+             "sha256": hashlib.sha256(img).hexdigest(), "crops": crops(img, w, h)}
+    if keep:
+        fn = f"render_{name}.rgb.gz"
+        with open(os.path.join(HERE, fn), "wb") as raw_f, gzip.GzipFile(fileobj=raw_f, mode="wb", compresslevel=9, mtime=0) as f:
+            f.write(img)
+        entry["file"] = fn
+    manifest["renders"][name] = entry
+    print(f"{name}: {w}x{h} sha256={entry['sha256'][:16]}", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    if not os.path.exists(REF):
+        sys.exit("oracle/_ref/ref_render missing: run `make -C oracle` where /root/reference exists")
+    mpath = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(mpath)) if os.path.exists(mpath) else {"renders": {}}
+    manifest["generator"] = ("oracle/_ref/ref_render: reference sources built with gcc -std=c11 -O2 -fopenmp "
+                             "(glibc 2.35 libm, FMA ifuncs); texture.c restated in oracle/ref_texture.c")
+    if not args.only:
+        kat = subprocess.run([REF, "kat"], capture_output=True, text=True, check=True).stdout
+        open(os.path.join(HERE, "kat.txt"), "w").write(kat)
+        for s in range(8):
+            d = subprocess.run([REF, "dump", str(s)], capture_output=True, text=True, check=True).stdout
+            with gzip.open(os.path.join(HERE, f"scene{s}.dump.gz"), "wt", compresslevel=9) as f:
+                f.write(d)
+        with tempfile.TemporaryDirectory() as td:
+            t = os.path.join(td, "x.tiff")
+            subprocess.run([REF, "render", "0", "400", "1", "1", t], capture_output=True, check=True)
+            data = open(t, "rb").read()
+            open(os.path.join(HERE, "tiff_header.bin"), "wb").write(data[:168])
+            manifest["tiff_s0_400x225_1spp_d1"] = {"size": len(data), "sha256": hashlib.sha256(data).hexdigest()}
+    todo = SMALL + BIG if (args.big or args.only) else SMALL
+    for cfg in todo:
+        if args.only and cfg[0] != args.only:
+            continue
+        render(*cfg, manifest)
+        json.dump(manifest, open(mpath, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

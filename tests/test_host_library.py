@@ -1,0 +1,186 @@
+"""Host side of the drop-in library (no GPU): scene construction, pcg32, TIFF bytes, C-ABI exports.
+
+The reference has no unit tests; its CI only builds and runs `./main 1` and `./main 4`
+(.github/workflows/build.yaml:20-21).  These tests check the pieces that must equal the
+reference bit for bit before any pixel is traced: the scene graph each of the 8 driver scenes
+builds (vs `ref_render dump`), the pcg32 stream (vs `ref_render kat`) and the TIFF writer.
+"""
+import ctypes
+import gzip
+import hashlib
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import pyoracle
+import rtc
+from conftest import GOLDEN, ROOT
+
+
+@pytest.mark.parametrize("scene", range(8))
+def test_scene_graph_matches_reference(scene, tmp_path):
+    """Same objects, materials, textures, BVH topology and camera as the reference's scene_<N>."""
+    sc = rtc.Scene.preset(scene)
+    mine = pyoracle.dump_flat(sc, str(tmp_path / "dump.txt"))
+    with gzip.open(os.path.join(GOLDEN, f"scene{scene}.dump.gz"), "rt") as f:
+        ref = f.read()
+    if mine != ref:
+        a, b = mine.splitlines(), ref.splitlines()
+        first = next(i for i in range(min(len(a), len(b))) if a[i] != b[i]) if a[:len(b)] != b[:len(a)] else min(len(a), len(b))
+        pytest.fail(f"scene {scene}: first difference at line {first}:\n mine: {a[first] if first < len(a) else None}\n"
+                    f"  ref: {b[first] if first < len(b) else None}")
+
+
+def _kat_lines():
+    return open(os.path.join(GOLDEN, "kat.txt")).read().splitlines()
+
+
+def test_pcg32_known_answers():
+    L = rtc.lib()
+
+    class PCG32(ctypes.Structure):
+        _fields_ = [("state", ctypes.c_uint64), ("inc", ctypes.c_uint64)]
+
+    L.pcg32_seed.argtypes = [ctypes.POINTER(PCG32), ctypes.c_uint64, ctypes.c_uint64]
+    L.pcg32_u32.argtypes = [ctypes.POINTER(PCG32)]
+    L.pcg32_u32.restype = ctypes.c_uint32
+    for line in _kat_lines():
+        m = re.match(r"seed (\d+) (\d+) state ([0-9a-f]+) inc ([0-9a-f]+) u32 (.*)", line)
+        if not m:
+            continue
+        g = PCG32()
+        L.pcg32_seed(ctypes.byref(g), int(m.group(1)), int(m.group(2)))
+        assert (g.state, g.inc) == (int(m.group(3), 16), int(m.group(4), 16))
+        got = [L.pcg32_u32(ctypes.byref(g)) for _ in range(8)]
+        assert got == [int(x, 16) for x in m.group(5).split()]
+
+
+def test_vec3_rand_draw_order_is_gcc_order():
+    """vec3_rand fills z with the first draw (gcc right-to-left argument evaluation)."""
+    L = rtc.lib()
+
+    class PCG32(ctypes.Structure):
+        _fields_ = [("state", ctypes.c_uint64), ("inc", ctypes.c_uint64)]
+
+    class Vec3(ctypes.Structure):
+        _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+    L.pcg32_seed.argtypes = [ctypes.POINTER(PCG32), ctypes.c_uint64, ctypes.c_uint64]
+    L.vec3_rand.argtypes = [ctypes.POINTER(PCG32)]
+    L.vec3_rand.restype = Vec3
+    L.vec3_rand_unit_vector.argtypes = [ctypes.POINTER(PCG32)]
+    L.vec3_rand_unit_vector.restype = Vec3
+    g = PCG32()
+    L.pcg32_seed(ctypes.byref(g), 19, 29)
+    v = L.vec3_rand(ctypes.byref(g))
+    u = L.vec3_rand_unit_vector(ctypes.byref(g))
+    kat = {l.split(")")[0] + ")": l.split(")")[1].split() for l in _kat_lines() if l.startswith("vec3_")}
+    assert [float.fromhex(x) for x in kat["vec3_rand(seed 19 29)"]] == [v.x, v.y, v.z]
+    assert [float.fromhex(x) for x in kat["vec3_rand_unit_vector(next)"]] == [u.x, u.y, u.z]
+
+
+def _write_tiff(w, h, n, data):
+    L = rtc.lib()
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    L.write_tiff.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.write_tiff.restype = ctypes.c_int
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "o.tiff")
+        f = libc.fopen(p.encode(), b"wb")
+        buf = np.ascontiguousarray(data, dtype=np.uint8)
+        rc = L.write_tiff(f, w, h, n, buf.ctypes.data)
+        libc.fclose(f)
+        return rc, open(p, "rb").read()
+
+
+def test_tiff_header_matches_reference():
+    rc, data = _write_tiff(400, 225, 3, np.zeros(400 * 225 * 3, np.uint8))
+    assert rc == 0
+    assert data[:168] == open(os.path.join(GOLDEN, "tiff_header.bin"), "rb").read()
+    assert len(data) == 168 + 400 * 225 * 3
+
+
+def test_tiff_full_file_matches_reference(manifest):
+    """Byte-identical TIFF for the reference's 400x225 1-spp depth-1 scene-0 render."""
+    e = manifest["tiff_s0_400x225_1spp_d1"]
+    sc = rtc.Scene.preset(0, 400, 1, 1)
+    img = pyoracle.render(sc)
+    rc, data = _write_tiff(400, 225, 3, img)
+    assert rc == 0 and len(data) == e["size"]
+    assert hashlib.sha256(data).hexdigest() == e["sha256"]
+
+
+def test_tiff_grayscale_and_unsupported_channels():
+    rc, data = _write_tiff(4, 2, 1, np.arange(8, dtype=np.uint8))
+    assert rc == 0 and len(data) == 146 + 2 + 16 + 8 and data[-8:] == bytes(range(8))
+    rc, data = _write_tiff(4, 2, 2, np.zeros(16, np.uint8))
+    assert rc == 1 and len(data) == 10 + 3 * 12  # the reference bails after the first 3 entries
+
+
+def _declared_functions():
+    names = set()
+    for fn in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        src = open(os.path.join(ROOT, "include", fn)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        src = re.sub(r"#[^\n]*(\\\n[^\n]*)*", "", src)  # macros (vec3_add etc. are macros)
+        src = re.sub(r"typedef struct \w+ \{.*?\} \w+;", "", src, flags=re.S)
+        src = re.sub(r"(struct|union|enum) \w* ?\{.*?\};", "", src, flags=re.S)
+        src = re.sub(r"typedef [^;]*;", "", src)
+        src = re.sub(r"static inline[^{]*\{[^}]*\}", "", src)
+        for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_function():
+    names = _declared_functions()
+    for must in ("Camera_render", "Camera_init", "World_init", "rt_render", "rt_render_rows_async",
+                 "rt_scene_upload", "rt_flatten", "write_tiff", "pcg32_seed", "BVHNode_new", "Perlin_new"):
+        assert must in names
+    L = rtc.lib()
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
+    assert hasattr(L, "VEC3_ZERO")
+
+
+def test_product_library_does_not_link_the_oracle():
+    out = subprocess.run(["ldd", rtc.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    syms = subprocess.run(["nm", "-D", "--defined-only", rtc.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in syms
+    assert rtc.lib().rt_abi_version() == 1
+
+
+def test_flattener_rejects_foreign_objects():
+    """An object whose vtable this library did not create fails loudly instead of rendering wrong."""
+    L = rtc.lib()
+    sc = rtc.Scene.preset(0, 40, 1, 1)
+    assert sc.features == 0 and sc.s.stack_needed >= 1
+    s1 = rtc.Scene.preset(1, 40, 1, 1)
+    assert s1.features & rtc.FEAT_BVH and s1.features & rtc.FEAT_DOF
+    s7 = rtc.Scene.preset(7, 40, 1, 1)
+    for f in (rtc.FEAT_QUAD, rtc.FEAT_XFORM, rtc.FEAT_MEDIUM, rtc.FEAT_LIGHTS, rtc.FEAT_TEX_UV, rtc.FEAT_TEX_PERLIN):
+        assert s7.features & f
+    assert s7.s.stack_needed <= 48
+    L.rt_flatten.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.rt_flatten.restype = ctypes.c_void_p
+    assert not L.rt_flatten(None, None)
+    assert "NULL" in rtc.last_error()
+
+
+def test_rows_partition_covers_frame_once():
+    for h in (1, 2, 7, 168, 675):
+        for world in (1, 2, 3, 4, 8):
+            rows = []
+            for r in range(world):
+                row0, stride, n = rtc.rows_of(h, r, world)
+                rows += [row0 + k * stride for k in range(n)]
+            assert sorted(rows) == list(range(h))

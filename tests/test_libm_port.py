@@ -1,0 +1,92 @@
+"""The glibc-exact libm port (ray-tracing-c_amd/csrc/rt_libm.h) against the host glibc the reference
+links, over the domains the hot path feeds it.
+
+CPU: the port compiled for the host (hipcc host pass), exhaustively:
+  sincosf on all 2^24 Lambertian/Sphere_rand angles phi = (2*(float)pi) * k/2^24
+  powf(x, 5) on every float in [0, 2]            (Dielectric Schlick term, src/material.c:73)
+  logf on all 2^24 pcg32_f32 values              (ConstantMedium, src/hittable.c:413)
+GPU: the same functions compiled for gfx950, on the same domains (pow5 strided), through the
+C ABI's rt_diag_libm, compared with glibc evaluated on the host.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import rtc
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, "tests", "native", "bin")
+
+
+@pytest.mark.parametrize("fn", ["sincos_phi", "pow5", "logf_f32"])
+def test_port_exhaustive_on_host(fn):
+    r = subprocess.run([os.path.join(BIN, "libm_check"), fn], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and " mismatches=0 " in r.stdout, r.stdout + r.stderr
+
+
+def test_port_sincos_large_arguments_sample_on_host():
+    """|x| >= 120 uses the 4/pi bit-table reduction (Perlin's sinf argument can get there)."""
+    lo, hi = 0x42f00000, 0x42f00000 + (1 << 22)
+    r = subprocess.run([os.path.join(BIN, "libm_check"), "sincos_all", hex(lo), hex(hi)], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0 and " mismatches=0 " in r.stdout, r.stdout + r.stderr
+
+
+def _glibc():
+    L = ctypes.CDLL(os.path.join(BIN, "libglibc_ref.so"))
+    for n in ("ref_sincosf", "ref_pow5", "ref_logf", "ref_sinf"):
+        getattr(L, n).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        getattr(L, n).restype = None
+    return L
+
+
+def _host(fn_name, x, nout):
+    out = np.empty(nout, np.float32)
+    getattr(_glibc(), fn_name)(x.ctypes.data, out.ctypes.data, x.size)
+    return out
+
+
+def _same_bits(a, b):
+    a, b = a.view(np.uint32), b.view(np.uint32)
+    nan = np.isnan(a.view(np.float32)) & np.isnan(b.view(np.float32))
+    return (a == b) | nan
+
+
+@pytest.mark.gpu
+def test_device_sincos_phi_domain_exhaustive():
+    k = np.arange(1 << 24, dtype=np.float32)
+    phi = np.float32(2.0 * np.float32(np.pi)) * (k / np.float32(1 << 24))
+    dev = rtc.diag_libm(0, phi)
+    host = _host("ref_sincosf", phi, 2 * phi.size)
+    ok = _same_bits(dev, host)
+    assert ok.all(), f"{(~ok).sum()} mismatches, first phi={phi[np.argmin(ok) // 2]!r}"
+
+
+@pytest.mark.gpu
+def test_device_logf_f32_domain_exhaustive():
+    x = (np.arange(1, 1 << 24, dtype=np.float64) / (1 << 24)).astype(np.float32)
+    ok = _same_bits(rtc.diag_libm(2, x), _host("ref_logf", x, x.size))
+    assert ok.all(), f"{(~ok).sum()} mismatches"
+
+
+@pytest.mark.gpu
+def test_device_pow5_unit_interval_strided():
+    bits = np.arange(0, 0x3F800001, 13, dtype=np.uint32)  # every 13th float in [0, 1]
+    x = bits.view(np.float32)
+    ok = _same_bits(rtc.diag_libm(1, x), _host("ref_pow5", x, x.size))
+    assert ok.all(), f"{(~ok).sum()} mismatches"
+
+
+@pytest.mark.gpu
+def test_device_sinf_random_and_special():
+    rng = np.random.default_rng(1)
+    bits = rng.integers(0, 1 << 32, 1 << 22, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(np.float32)
+    x = x[np.isfinite(x)]
+    specials = np.array([0.0, -0.0, 1e-30, 120.0, -120.0, 1e10, 3.4e38, np.pi, 2 * np.pi], np.float32)
+    x = np.concatenate([x, specials]).astype(np.float32)
+    ok = _same_bits(rtc.diag_libm(3, x), _host("ref_sinf", x, x.size))
+    assert ok.all(), f"{(~ok).sum()} mismatches, first x={x[np.argmin(ok)]!r}"
