@@ -176,11 +176,8 @@ def main():
         else:
             parts = [rows]
         if rank == 0:
-            frame = torch.empty((H, W, 3), dtype=torch.uint8)
-            for r, p in enumerate(parts):
-                r0, st, n = rtc.rows_of(H, r, world)
-                frame[r0::st][:n] = p[:n].cpu()
-            sha = hashlib.sha256(frame.numpy().tobytes()).hexdigest()
+            frame = rtc.assemble_frame([p.cpu().numpy() for p in parts], H, world)
+            sha = hashlib.sha256(frame.tobytes()).hexdigest()
             name, g = golden_for(args)
             parity = {"frame_sha256": sha, "golden": name,
                       "pixel_identical_to_reference": (sha == g["sha256"]) if g else None,

@@ -21,11 +21,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/rt_flat.h"
 #include "rt_libm.h"
 
-#define RT_D __device__ __forceinline__
+// Device code is also compiled for the host by the test-only harness tests/native/kernel_host_check.cpp
+// (AddressSanitizer + comparison with the oracle before anything runs on a GPU).
+#define RT_D __host__ __device__ __forceinline__
 
 namespace rt {
 
@@ -104,6 +107,36 @@ struct DScene {
   const uint8_t *image_bytes;
   int32_t n_textures, n_images;
 };
+
+// Kernel variants compiled per feature set; a scene runs on the smallest variant covering it.
+constexpr int kFeatBook1 = RT_FEAT_BVH | RT_FEAT_DOF;  // spheres, lists, BVH: scenes 0 and 1
+constexpr int kFeatAll = 0x1ff;
+
+// A DScene whose arrays are the given (host or device) copies of the flat scene's arrays.
+inline DScene make_view(const rt_flat_scene &s, const void *const arrays[13]) {
+  DScene v;
+  memset(&v, 0, sizeof v);
+  v.cam = s.camera;
+  v.root = s.root;
+  v.lights = s.lights;
+  v.features = s.features;
+  v.bvh = (const rt_bvh_node *)arrays[0];
+  v.spheres = (const rt_sphere *)arrays[1];
+  v.quads = (const rt_quad *)arrays[2];
+  v.lists = (const rt_list *)arrays[3];
+  v.items = (const int32_t *)arrays[4];
+  v.translates = (const rt_translate *)arrays[5];
+  v.rotates = (const rt_rotate_y *)arrays[6];
+  v.media = (const rt_medium *)arrays[7];
+  v.materials = (const rt_material *)arrays[8];
+  v.textures = (const rt_texture *)arrays[9];
+  v.images = (const rt_image *)arrays[10];
+  v.perlins = (const rt_perlin *)arrays[11];
+  v.image_bytes = (const uint8_t *)arrays[12];
+  v.n_textures = s.n_textures;
+  v.n_images = s.n_images;
+  return v;
+}
 
 // ------------------------------------------------------------------------------ primitives
 // Sphere_hit up to the accepted root (src/hittable.c:120-138); a = |d|^2 hoisted per ray.
@@ -218,7 +251,13 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
   // of any length costs one stack slot (need computed by rt_flatten.c: stack_need)
   uint64_t stack[kStackMax];
   int sp = 0;
-  stack[sp++] = (uint32_t)S.root;
+  // pushes are bounds-checked for memory safety only: rt_scene_upload rejects scenes whose
+  // computed stack need exceeds kStackMax, so the guard never fires on a validated scene
+#define RT_PUSH(x)                                                                                 \
+  do {                                                                                             \
+    if (sp < kStackMax) stack[sp++] = (x);                                                         \
+  } while (0)
+  RT_PUSH((uint32_t)S.root);
   float tmax = __builtin_inff();
   bool found = false;
   int32_t frame = RT_REF_NONE;
@@ -233,8 +272,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
     if ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) {
       const rt_bvh_node &n = S.bvh[idx];
       if (aabb_hit(n, o, inv, tmin, tmax)) {
-        if (n.right != RT_REF_NONE) stack[sp++] = (uint32_t)n.right;
-        stack[sp++] = (uint32_t)n.left;
+        if (n.right != RT_REF_NONE) RT_PUSH((uint32_t)n.right);
+        RT_PUSH((uint32_t)n.left);
       }
     } else if (kind == RT_KIND_SPHERE) {
       float t;
@@ -249,8 +288,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
       const rt_list l = S.lists[idx];
       const int32_t pos = (int32_t)(e >> 32);
       if (pos < l.count) {
-        if (pos + 1 < l.count) stack[sp++] = (uint32_t)ref | ((uint64_t)(pos + 1) << 32);
-        stack[sp++] = (uint32_t)S.items[l.first + pos];
+        if (pos + 1 < l.count) RT_PUSH((uint32_t)ref | ((uint64_t)(pos + 1) << 32));
+        RT_PUSH((uint32_t)S.items[l.first + pos]);
       }
     } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
       float t;
@@ -262,8 +301,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
         found = true;
       }
     } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
-      stack[sp++] = (uint32_t)rt_ref(kExitTag, 0) | ((uint64_t)(uint32_t)ref << 32);
-      stack[sp++] = (uint32_t)(kind == RT_KIND_TRANSLATE ? S.translates[idx].child : S.rotates[idx].child);
+      RT_PUSH((uint32_t)rt_ref(kExitTag, 0) | ((uint64_t)(uint32_t)ref << 32));
+      RT_PUSH((uint32_t)(kind == RT_KIND_TRANSLATE ? S.translates[idx].child : S.rotates[idx].child));
       frame = ref;
       local_ray(S, frame, wo, wd, o, d);
       inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -298,6 +337,7 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
       }
     }
   }
+#undef RT_PUSH
   return found;
 }
 
@@ -391,8 +431,8 @@ RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p) {
       const rt_image im = S.images[t.a];
       int i = (int)roundf(u * (float)(im.width - 1));
       int j = (int)roundf((1.0f - v) * (float)(im.height - 1));
-      i = min(max(i, 0), im.width - 1);  // memory safety only: in range for u,v in [0,1]
-      j = min(max(j, 0), im.height - 1);
+      i = i < 0 ? 0 : (i > im.width - 1 ? im.width - 1 : i);  // memory safety only: in range for
+      j = j < 0 ? 0 : (j > im.height - 1 ? im.height - 1 : j);  // u,v in [0,1]
       const uint8_t *px = S.image_bytes + im.offset + ((int64_t)j * im.width + i) * 3;
       return mk((float)px[0] / 255.0f, (float)px[1] / 255.0f, (float)px[2] / 255.0f);
     }
@@ -600,7 +640,9 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
     rec_a[n] = albedo;
     if (kFull) {
       rec_e[n] = e;
-      if ((F & RT_FEAT_LIGHTS) && !skip_pdf) {  // mixture pdf (src/raytracing.c:61-71)
+      // mixture pdf (src/raytracing.c:56-71): only when the scene has lights and p != 0 (runtime bit:
+      // a kernel variant compiled with the LIGHTS path may run a scene without lights)
+      if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
         if (g.f32() < prob) out = lights_rand(S, r.p, g);
         const float sp = scatter_pdf(S, r.material, r.normal, out);
         const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, out);
@@ -623,6 +665,43 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
     }
   }
   return c;
+}
+
+// ------------------------------------------------------------------------------ one pixel
+// Camera_render's per-pixel body (src/raytracing.c:93-131): seed, spp samples (jitter, thin-lens
+// disc, primary ray, path colour), mean, gamma 2, clamp-macro semantics (NaN -> 0), truncation.
+template <int F>
+RT_D void render_pixel(const DScene &S, int i, int j, uint8_t *dst) {
+  Pcg32 g;
+  g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));
+  const f3 du = ld3(S.cam.delta_u), dv = ld3(S.cam.delta_v), lf = ld3(S.cam.origin);
+  const f3 pixel_pos = add(add(ld3(S.cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+  const bool dof = S.cam.dof_angle > 0.0f;
+  f3 acc = mk(0.0f, 0.0f, 0.0f);
+  for (int s = 0; s < S.cam.spp; s++) {
+    const float px = g.between(-0.5f, 0.5f);
+    const float py = g.between(-0.5f, 0.5f);
+    f3 o = lf;
+    if (dof) {  // thin-lens disc by rejection (src/raytracing.c:108-117)
+      float a, b;
+      for (;;) {
+        a = g.between(-1.0f, 1.0f);
+        b = g.between(-1.0f, 1.0f);
+        if (a * a + b * b < 1.0f) break;
+      }
+      o = add(add(lf, scale(ld3(S.cam.disc_u), a)), scale(ld3(S.cam.disc_v), b));
+    }
+    const f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+    acc = add(acc, path_color<F>(S, o, d, g));
+  }
+  const float spp_f = (float)S.cam.spp;
+  const float ch[3] = {acc.x, acc.y, acc.z};
+  for (int c = 0; c < 3; c++) {
+    float v = sqrtf(ch[c] / spp_f);
+    v = v > 0.0f ? v : 0.0f;
+    v = v < 0.999f ? v : 0.999f;
+    dst[c] = (uint8_t)(int)(256.0f * v);
+  }
 }
 
 }  // namespace rt

@@ -46,10 +46,7 @@ extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 // ------------------------------------------------------------------------------ kernels
 constexpr int kBlock = 256;
-constexpr int kFeatBook1 = RT_FEAT_BVH | RT_FEAT_DOF;  // spheres, lists, BVH: scenes 0 and 1
-constexpr int kFeatAll = 0x1ff;
 
-// Camera_render's per-pixel body (src/raytracing.c:93-131).
 template <int F>
 __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int row0, int row_stride, int n_rows,
                                                                 uint8_t *__restrict__ out) {
@@ -58,40 +55,7 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
   if (pix >= (int64_t)n_rows * W) return;
   const int jj = (int)(pix / W);
   const int i = (int)(pix - (int64_t)jj * W);
-  const int j = row0 + jj * row_stride;
-
-  Pcg32 g;
-  g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));
-  const f3 du = ld3(S.cam.delta_u), dv = ld3(S.cam.delta_v), lf = ld3(S.cam.origin);
-  const f3 pixel_pos = add(add(ld3(S.cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
-  const bool dof = S.cam.dof_angle > 0.0f;
-  f3 acc = mk(0.0f, 0.0f, 0.0f);
-  for (int s = 0; s < S.cam.spp; s++) {
-    const float px = g.between(-0.5f, 0.5f);
-    const float py = g.between(-0.5f, 0.5f);
-    f3 o = lf;
-    if (dof) {  // thin-lens disc by rejection (src/raytracing.c:108-117)
-      float a, b;
-      for (;;) {
-        a = g.between(-1.0f, 1.0f);
-        b = g.between(-1.0f, 1.0f);
-        if (a * a + b * b < 1.0f) break;
-      }
-      o = add(add(lf, scale(ld3(S.cam.disc_u), a)), scale(ld3(S.cam.disc_v), b));
-    }
-    const f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
-    acc = add(acc, path_color<F>(S, o, d, g));
-  }
-  const float spp_f = (float)S.cam.spp;
-  const float ch[3] = {acc.x, acc.y, acc.z};
-  uint8_t *dst = out + pix * 3;
-#pragma unroll
-  for (int c = 0; c < 3; c++) {  // gamma 2 + clamp macro semantics (NaN -> 0) + truncation
-    float v = sqrtf(ch[c] / spp_f);
-    v = v > 0.0f ? v : 0.0f;
-    v = v < 0.999f ? v : 0.999f;
-    dst[c] = (uint8_t)(int)(256.0f * v);
-  }
+  render_pixel<F>(S, i, row0 + jj * row_stride, out + pix * 3);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -258,28 +222,9 @@ extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) 
   d->features = s->features;
   d->width = s->camera.width;
   d->height = s->camera.height;
-  DScene &v = d->view;
-  memset(&v, 0, sizeof v);
-  v.cam = s->camera;
-  v.root = s->root;
-  v.lights = s->lights;
-  v.features = s->features;
-  char *b = (char *)arena;
-  v.bvh = (const rt_bvh_node *)(b + parts[0].off);
-  v.spheres = (const rt_sphere *)(b + parts[1].off);
-  v.quads = (const rt_quad *)(b + parts[2].off);
-  v.lists = (const rt_list *)(b + parts[3].off);
-  v.items = (const int32_t *)(b + parts[4].off);
-  v.translates = (const rt_translate *)(b + parts[5].off);
-  v.rotates = (const rt_rotate_y *)(b + parts[6].off);
-  v.media = (const rt_medium *)(b + parts[7].off);
-  v.materials = (const rt_material *)(b + parts[8].off);
-  v.textures = (const rt_texture *)(b + parts[9].off);
-  v.images = (const rt_image *)(b + parts[10].off);
-  v.perlins = (const rt_perlin *)(b + parts[11].off);
-  v.image_bytes = (const uint8_t *)(b + parts[12].off);
-  v.n_textures = s->n_textures;
-  v.n_images = s->n_images;
+  const void *dev_arrays[13];
+  for (int k = 0; k < 13; k++) dev_arrays[k] = (char *)arena + parts[k].off;
+  d->view = make_view(*s, dev_arrays);
   return d;
 }
 

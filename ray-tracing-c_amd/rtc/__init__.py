@@ -216,6 +216,16 @@ def rows_of(height: int, rank: int, world: int):
     return rank, world, max(n, 0)
 
 
+def assemble_frame(parts, height: int, world: int) -> np.ndarray:
+    """Inverse of rows_of: parts[r] holds rank r's rows (possibly padded); returns (H, W, 3)."""
+    first = np.asarray(parts[0])
+    frame = np.empty((height,) + first.shape[1:], dtype=first.dtype)
+    for r, p in enumerate(parts):
+        row0, stride, n = rows_of(height, r, world)
+        frame[row0::stride][:n] = np.asarray(p)[:n]
+    return frame
+
+
 def diag_libm(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:
     """Evaluate the device libm port (0 sincosf, 1 powf(x,5), 2 logf, 3 sinf) on float32 inputs."""
     x = np.ascontiguousarray(x, dtype=np.float32)
