@@ -1,0 +1,350 @@
+// rt_book1.h — the fast path for sphere/BVH scenes (reference scenes 0 and 1: the headline
+// Book-1 final scene).  Same arithmetic as rt_device.h (bit-exact with the reference); different
+// execution structure, designed for a 64-wide CDNA4 wavefront:
+//
+//  * persistent lanes + wave-level work stealing: a lane that finishes its pixel takes the next
+//    unrendered pixel (one atomic per wave per refill: ballot + mbcnt), so the frame has no tail of
+//    half-empty waves and no per-pixel load imbalance (sky vs ground rows);
+//  * one flattened loop per lane over (sample, bounce): every iteration a lane traces one ray;
+//    lanes whose path ended generate their next camera ray in the same iteration, so a wave never
+//    waits for its longest path at a sample boundary (Camera_ray_color's recursion, unrolled);
+//  * BVH nodes and sphere (center, r^2) staged once per workgroup in LDS; per-lane DFS stack in LDS
+//    ([slot][lane], 16-bit refs: conflict-free); traversal keeps the reference's left-then-right
+//    order and shrinking t_max, tests leaf spheres inline, and never pushes the left child;
+//  * the path record is a list of material ids (albedo of a Solid texture is a function of the
+//    material) in registers (kRecRegs slots) + a per-lane global spill area for deep paths; the
+//    colour is folded innermost-first at path end exactly like the recursion.
+//
+// Eligibility (host-checked, rt_kernel.hip: book1_eligible): spheres only, BVH nodes, lists only at
+// the root, Lambertian/Metal/Dielectric with Solid albedo, no lights/emission/textures/transforms.
+#pragma once
+#include "rt_device.h"
+
+namespace rt {
+namespace b1 {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kStackSlots = 16;   // per-lane DFS slots in LDS, 32-bit (host checks the need)
+constexpr int kRecRegs = 8;       // path-record slots held in registers (4 x 16-bit per u64)
+constexpr uint16_t kLeafBit = 0x8000;  // 16-bit ref: leaf sphere index | kLeafBit, else node index
+
+struct FastMat {   // 32 B: material resolved to what the Book-1 path needs
+  float albedo[3];  // Solid texture colour; (1,1,1) for Dielectric
+  float param;      // fuzz / eta
+  int32_t tag;
+  int32_t pad[3];
+};
+
+struct Book1View {
+  DScene S;                  // full scene (global memory): sphere aux data, camera
+  const float4 *nodes_g;     // 2 float4 per node: (lo.xyz, left as int bits), (hi.xyz, right bits)
+  const float4 *spheres_g;   // (center.xyz, r^2)
+  const FastMat *mats;
+  const uint16_t *root_items;
+  int32_t n_nodes, n_spheres, n_root;
+  int32_t stack_need;
+  int32_t row0, row_stride, n_rows;
+  int32_t *work_counter;     // zeroed before each launch
+  uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
+  int32_t spill_lanes;
+};
+
+// ---------------------------------------------------------------- wave helpers
+RT_D int lane_id() { return __lane_id(); }
+
+// ---------------------------------------------------------------- traversal
+struct TraceState {
+  f3 o, d, inv;
+  float a;       // |d|^2
+  float tmax;
+  int32_t hit;   // sphere index or -1
+};
+
+RT_D void sphere_test_lds(const float4 *sph, int idx, TraceState &T, float tmin) {
+  const float4 s = sph[idx];
+  const f3 oc = sub(T.o, mk(s.x, s.y, s.z));
+  const float b = dot(oc, T.d);
+  const float c = dot(oc, oc) - s.w;
+  const float disc = b * b - T.a * c;
+  if (disc < 0) return;
+  const float sq = sqrtf(disc);
+  float root = (-b - sq) / T.a;
+  if (root <= tmin || root >= T.tmax) {
+    root = (-b + sq) / T.a;
+    if (root <= tmin || root >= T.tmax) return;
+  }
+  T.tmax = root;
+  T.hit = idx;
+}
+
+RT_D bool aabb_lds(float4 lo, float4 hi, const TraceState &T, float tmin) {
+  // AABB_hit (src/hittable.c:38-55), slab by slab with the reference's early exit
+  float tmax = T.tmax;
+  {
+    float t0 = (lo.x - T.o.x) * T.inv.x, t1 = (hi.x - T.o.x) * T.inv.x;
+    if (T.inv.x < 0) { const float s = t0; t0 = t1; t1 = s; }
+    tmin = fmaxf(tmin, t0);
+    tmax = fminf(tmax, t1);
+    if (tmax <= tmin) return false;
+  }
+  {
+    float t0 = (lo.y - T.o.y) * T.inv.y, t1 = (hi.y - T.o.y) * T.inv.y;
+    if (T.inv.y < 0) { const float s = t0; t0 = t1; t1 = s; }
+    tmin = fmaxf(tmin, t0);
+    tmax = fminf(tmax, t1);
+    if (tmax <= tmin) return false;
+  }
+  {
+    float t0 = (lo.z - T.o.z) * T.inv.z, t1 = (hi.z - T.o.z) * T.inv.z;
+    if (T.inv.z < 0) { const float s = t0; t0 = t1; t1 = s; }
+    tmin = fmaxf(tmin, t0);
+    tmax = fminf(tmax, t1);
+    if (tmax <= tmin) return false;
+  }
+  return true;
+}
+
+// Closest hit of World.objects (a root list of BVH roots / spheres) in [tmin, inf).
+RT_D void trace(const Book1View &V, const float4 *nodes, const float4 *sph, uint32_t *stack, int lane_stride,
+                TraceState &T, float tmin) {
+  T.tmax = __builtin_inff();
+  T.hit = -1;
+  for (int k = 0; k < V.n_root; k++) {  // root list, in order (wave-uniform loop)
+    uint32_t cur = V.root_items[k];
+    int sp = 0;
+    for (;;) {
+      if (cur & kLeafBit) {
+        sphere_test_lds(sph, (int)(cur & 0x7fff), T, tmin);
+      } else {
+        const float4 lo = nodes[2 * cur], hi = nodes[2 * cur + 1];
+        if (aabb_lds(lo, hi, T, tmin)) {
+          const uint32_t l = __float_as_uint(lo.w), r = __float_as_uint(hi.w);
+          if (l & kLeafBit) {
+            sphere_test_lds(sph, (int)(l & 0x7fff), T, tmin);
+            if (r != 0xffffu) {
+              if (r & kLeafBit) {
+                sphere_test_lds(sph, (int)(r & 0x7fff), T, tmin);
+              } else {
+                cur = r;
+                continue;
+              }
+            }
+          } else {
+            if (r != 0xffffu) {
+              stack[sp * lane_stride] = r;
+              sp++;
+            }
+            cur = l;
+            continue;
+          }
+        }
+      }
+      if (sp == 0) break;
+      sp--;
+      cur = stack[sp * lane_stride];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- path record
+struct Record {
+  uint64_t r0, r1;  // 8 x 16-bit material ids, newest in the low bits of r0
+  int n;
+};
+
+RT_D void rec_push(const Book1View &V, Record &R, uint32_t id, int glane) {
+  if (R.n >= kRecRegs) {  // oldest register slot moves to the spill area (rare: deep paths)
+    const uint16_t oldest = (uint16_t)(R.r1 >> 48);
+    V.spill[(int64_t)(R.n - kRecRegs) * V.spill_lanes + glane] = oldest;
+  }
+  R.r1 = (R.r1 << 16) | (R.r0 >> 48);
+  R.r0 = (R.r0 << 16) | id;
+  R.n++;
+}
+
+// c = a_k * c for k = n-1 .. 0 (newest first), the recursion's evaluation order
+RT_D f3 rec_fold(const Book1View &V, const Record &R, f3 c, int glane) {
+  uint64_t r0 = R.r0, r1 = R.r1;
+  const int in_regs = R.n < kRecRegs ? R.n : kRecRegs;
+  for (int k = 0; k < in_regs; k++) {
+    const FastMat &m = V.mats[(uint32_t)(r0 & 0xffff)];
+    c = add(mk(0.0f, 0.0f, 0.0f), mul(ld3(m.albedo), c));
+    r0 = (r0 >> 16) | (r1 << 48);
+    r1 >>= 16;
+  }
+  for (int k = R.n - kRecRegs - 1; k >= 0; k--) {
+    const FastMat &m = V.mats[V.spill[(int64_t)k * V.spill_lanes + glane]];
+    c = add(mk(0.0f, 0.0f, 0.0f), mul(ld3(m.albedo), c));
+  }
+  return c;
+}
+
+// ---------------------------------------------------------------- scattering (Book-1 materials)
+RT_D f3 scatter(const FastMat &m, f3 normal, bool front, f3 r_in, Pcg32 &g) {
+  if (m.tag == RT_MAT_LAMBERTIAN) {  // src/material.c:23-37
+    const Onb b = onb_from_w(normal);
+    const float r1 = g.f32();
+    const float r2 = g.f32();
+    const float phi = (2.0f * kPi) * r1;
+    float sphi, cphi;
+    rtm::sincosf(phi, &sphi, &cphi);
+    const float sq = sqrtf(r2);
+    return onb_local(b, mk(cphi * sq, sphi * sq, sqrtf(1.0f - r2)));
+  }
+  if (m.tag == RT_MAT_METAL) {  // src/material.c:48-58
+    const f3 refl = reflect(normalize(r_in), normal);
+    const f3 out = add(refl, scale(rand_unit_vector(g), m.param));
+    return dot(out, normal) < 0.0f ? refl : out;
+  }
+  // DIELECTRIC, src/material.c:62-86
+  float eta = m.param;
+  if (front) eta = 1.0f / eta;
+  const f3 v = normalize(r_in);
+  const float cos_t = fminf(-dot(v, normal), 1.0f);
+  const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+  float sch = (1.0f - eta) / (1.0f + eta);
+  sch *= sch;
+  sch += (1 - sch) * rtm::powf(1.0f - cos_t, 5.0f);
+  if (eta * sin_t > 1.0f || sch > g.f32()) return reflect(v, normal);
+  const f3 perp = scale(add(v, scale(normal, cos_t)), eta);
+  const f3 para = scale(normal, -sqrtf(fabsf(1.0f - dot(perp, perp))));
+  return add(perp, para);
+}
+
+// ---------------------------------------------------------------- the persistent kernel body
+template <bool kLds>
+__device__ void render(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
+  const int tid = threadIdx.x;
+  const int W = V.S.cam.width;
+  const int64_t total = (int64_t)V.n_rows * W;
+
+  // stage the scene (nodes + spheres) in LDS once per workgroup
+  // (when !kLds the stack still lives in LDS; only the scene arrays are read from global memory)
+  float4 *nodes = (float4 *)lds;
+  float4 *sph = nodes + (kLds ? 2 * V.n_nodes : 0);
+  uint32_t *stack_base = (uint32_t *)(sph + (kLds ? V.n_spheres : 0));
+  if (kLds) {
+    for (int k = tid; k < 2 * V.n_nodes; k += kBlock) nodes[k] = V.nodes_g[k];
+    for (int k = tid; k < V.n_spheres; k += kBlock) sph[k] = V.spheres_g[k];
+    __syncthreads();
+  } else {
+    nodes = (float4 *)V.nodes_g;
+    sph = (float4 *)V.spheres_g;
+  }
+  uint32_t *stack = stack_base + tid;  // slot k of this lane at stack[k * kBlock]: conflict-free
+  const int glane = blockIdx.x * kBlock + tid;
+  const int lane = lane_id();
+
+  const rt_camera &cam = V.S.cam;
+  const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
+  const f3 disc_u = ld3(cam.disc_u), disc_v = ld3(cam.disc_v), bg = ld3(cam.background);
+  const bool dof = cam.dof_angle > 0.0f;
+  const int spp = cam.spp, max_depth = cam.max_depth;
+  const float tmin = 1e-3f;
+
+  int64_t pix = -1;  // current work item (index into this launch's rows)
+  int i = 0, j = 0, s = 0, depth = 0;
+  bool need_pixel = true, need_sample = true;
+  Pcg32 g;
+  g.state = 0;
+  g.inc = 0;
+  f3 pixel_pos = mk(0, 0, 0), acc = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0);
+  Record R;
+  R.r0 = R.r1 = 0;
+  R.n = 0;
+
+  for (;;) {
+    // ---- refill: lanes without a pixel take consecutive work items, one atomic per wave
+    const uint64_t want = __ballot(need_pixel);
+    if (want) {
+      const int first = __builtin_ctzll(want);
+      int base = 0;
+      if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
+      base = __shfl(base, first);
+      if (need_pixel) {
+        const int rank_in_wave = __popcll(want & ((1ull << lane) - 1));
+        pix = base + rank_in_wave;
+        if (pix >= total) break;  // no work left for this lane
+        const int jj = (int)(pix / W);
+        i = (int)(pix - (int64_t)jj * W);
+        j = V.row0 + jj * V.row_stride;
+        g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
+        pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+        acc = mk(0.0f, 0.0f, 0.0f);
+        s = 0;
+        need_pixel = false;
+        need_sample = true;
+      }
+    }
+    // ---- camera ray for the next sample (src/raytracing.c:100-122)
+    if (need_sample) {
+      const float px = g.between(-0.5f, 0.5f);
+      const float py = g.between(-0.5f, 0.5f);
+      o = lf;
+      if (dof) {
+        float a, b;
+        for (;;) {
+          a = g.between(-1.0f, 1.0f);
+          b = g.between(-1.0f, 1.0f);
+          if (a * a + b * b < 1.0f) break;
+        }
+        o = add(add(lf, scale(disc_u, a)), scale(disc_v, b));
+      }
+      d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+      depth = max_depth;
+      R.n = 0;
+      need_sample = false;
+    }
+    // ---- one bounce (Camera_ray_color body, src/raytracing.c:39-75)
+    bool path_done = false;
+    f3 tail = mk(0.0f, 0.0f, 0.0f);
+    if (depth <= 0) {
+      path_done = true;
+    } else {
+      TraceState T;
+      T.o = o;
+      T.d = d;
+      T.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+      T.a = dot(d, d);
+      trace(V, nodes, sph, stack, kBlock, T, tmin);
+      if (T.hit < 0) {
+        tail = bg;
+        path_done = true;
+      } else {
+        const rt_sphere &sp = V.S.spheres[T.hit];
+        const f3 p = ray_at(o, d, T.tmax);
+        const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
+        const bool front = dot(d, outward) < 0.0f;
+        const f3 normal = front ? outward : neg(outward);
+        const FastMat &m = V.mats[sp.material];
+        const f3 nd = scatter(m, normal, front, d, g);
+        rec_push(V, R, (uint32_t)sp.material, glane);
+        o = p;
+        d = nd;
+        depth--;
+      }
+    }
+    if (path_done) {
+      acc = add(acc, rec_fold(V, R, tail, glane));
+      s++;
+      if (s == spp) {  // quantize (src/raytracing.c:127-131)
+        const float spp_f = (float)spp;
+        const float ch[3] = {acc.x, acc.y, acc.z};
+        uint8_t *dst = out + pix * 3;
+        for (int c = 0; c < 3; c++) {
+          float v = sqrtf(ch[c] / spp_f);
+          v = v > 0.0f ? v : 0.0f;
+          v = v < 0.999f ? v : 0.999f;
+          dst[c] = (uint8_t)(int)(256.0f * v);
+        }
+        need_pixel = true;
+      } else {
+        need_sample = true;
+      }
+    }
+  }
+}
+
+}  // namespace b1
+}  // namespace rt

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/rt_hip.h"
+#include "rt_book1.h"
 #include "rt_device.h"
 
 using namespace rt;
@@ -58,6 +59,13 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
   render_pixel<F>(S, i, row0 + jj * row_stride, out + pix * 3);
 }
 
+// Persistent Book-1 kernel (rt_book1.h): grid = resident workgroups, lanes steal pixels.
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  b1::render<kLds>(V, out, lds);
+}
+
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -84,6 +92,13 @@ struct rt_device_scene {
   size_t arena_bytes;
   int features;
   int width, height;
+  // Book-1 fast path (rt_book1.h), when the scene qualifies
+  bool book1 = false;
+  bool book1_lds = false;
+  b1::Book1View b1view;
+  void *b1_arena = nullptr;
+  int b1_grid = 0;
+  size_t b1_lds_bytes = 0;
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -168,11 +183,162 @@ static int validate(const rt_flat_scene *s) {
   return 0;
 }
 
+// ------------------------------------------------------------------------------ Book-1 packing
+static bool env_flag(const char *name, bool dflt) {
+  const char *e = getenv(name);
+  if (!e || !*e) return dflt;
+  return !(e[0] == '0' || e[0] == 'n' || e[0] == 'N' || e[0] == 'f' || e[0] == 'F');
+}
+
+// 16-bit ref used by the fast traversal: node index, or sphere index | 0x8000, or 0xffff (none)
+static bool pack_ref(int32_t ref, uint32_t *out) {
+  if (ref == RT_REF_NONE) return *out = 0xffffu, true;
+  const int32_t i = rt_ref_index(ref);
+  if (rt_ref_kind(ref) == RT_KIND_BVH && i < 0x7fff) return *out = (uint32_t)i, true;
+  if (rt_ref_kind(ref) == RT_KIND_SPHERE && i < 0x7fff) return *out = (uint32_t)i | b1::kLeafBit, true;
+  return false;
+}
+
+// stack slots the fast traversal needs below `ref` (rt_book1.h: trace never pushes a left child)
+static int b1_stack_need(const rt_flat_scene *s, int32_t ref, int depth_guard) {
+  if (ref == RT_REF_NONE || rt_ref_kind(ref) != RT_KIND_BVH || depth_guard > 4096) return 0;
+  const rt_bvh_node &n = s->bvh[rt_ref_index(ref)];
+  const bool left_leaf = rt_ref_kind(n.left) == RT_KIND_SPHERE;
+  if (left_leaf) return b1_stack_need(s, n.right, depth_guard + 1);
+  if (n.right == RT_REF_NONE) return b1_stack_need(s, n.left, depth_guard + 1);
+  const int l = 1 + b1_stack_need(s, n.left, depth_guard + 1), r = b1_stack_need(s, n.right, depth_guard + 1);
+  return l > r ? l : r;
+}
+
+static float bits_as_float(uint32_t u) {
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static bool book1_eligible(const rt_flat_scene *s) {
+  if (s->features & ~kFeatBook1) return false;
+  if (s->n_lists != 2 || s->n_quads || s->n_translates || s->n_rotates || s->n_media) return false;  // root + lights
+  if (s->lists[s->lights].count != 0) return false;
+  if (s->n_spheres >= 0x7fff || s->n_bvh >= 0x7fff || s->camera.max_depth > kMaxDepth) return false;
+  for (int k = 0; k < s->n_materials; k++) {
+    const rt_material &m = s->materials[k];
+    if (m.tag != RT_MAT_LAMBERTIAN && m.tag != RT_MAT_METAL && m.tag != RT_MAT_DIELECTRIC) return false;
+    if (m.tag != RT_MAT_DIELECTRIC && s->textures[m.texture].kind != RT_TEX_SOLID) return false;
+  }
+  for (int k = 0; k < s->n_bvh; k++) {
+    uint32_t a, b;
+    if (!pack_ref(s->bvh[k].left, &a) || !pack_ref(s->bvh[k].right, &b) || a == 0xffffu) return false;
+  }
+  const rt_list &root = s->lists[rt_ref_index(s->root)];
+  for (int k = 0; k < root.count; k++) {
+    uint32_t a;
+    if (!pack_ref(s->list_items[root.first + k], &a) || a == 0xffffu) return false;
+    if (b1_stack_need(s, s->list_items[root.first + k], 0) > b1::kStackSlots) return false;
+  }
+  return env_flag("RT_BOOK1", true);
+}
+
+// Build and upload the Book-1 arrays; sets d->book1 on success (failure just keeps the general path).
+static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
+  const rt_list &root = s->lists[rt_ref_index(s->root)];
+  std::vector<float4> nodes(2 * (size_t)s->n_bvh);
+  for (int k = 0; k < s->n_bvh; k++) {
+    const rt_bvh_node &n = s->bvh[k];
+    uint32_t l, r;
+    pack_ref(n.left, &l);
+    pack_ref(n.right, &r);
+    nodes[2 * k] = make_float4(n.lo[0], n.lo[1], n.lo[2], bits_as_float(l));
+    nodes[2 * k + 1] = make_float4(n.hi[0], n.hi[1], n.hi[2], bits_as_float(r));
+  }
+  std::vector<float4> sph(s->n_spheres);
+  for (int k = 0; k < s->n_spheres; k++)
+    sph[k] = make_float4(s->spheres[k].center[0], s->spheres[k].center[1], s->spheres[k].center[2],
+                         s->spheres[k].radius_sq);
+  std::vector<b1::FastMat> mats(s->n_materials);
+  for (int k = 0; k < s->n_materials; k++) {
+    const rt_material &m = s->materials[k];
+    b1::FastMat f;
+    memset(&f, 0, sizeof f);
+    f.tag = m.tag;
+    f.param = m.param;
+    if (m.tag == RT_MAT_DIELECTRIC) {
+      f.albedo[0] = f.albedo[1] = f.albedo[2] = 1.0f;  // Dielectric_scatter: *color = vec3(1, 1, 1)
+    } else {
+      const rt_texture &t = s->textures[m.texture];
+      f.albedo[0] = t.color[0];
+      f.albedo[1] = t.color[1];
+      f.albedo[2] = t.color[2];
+    }
+    mats[k] = f;
+  }
+  std::vector<uint16_t> roots(root.count > 0 ? root.count : 1);
+  int need = 0;
+  for (int k = 0; k < root.count; k++) {
+    uint32_t a;
+    pack_ref(s->list_items[root.first + k], &a);
+    roots[k] = (uint16_t)a;
+    const int nk = b1_stack_need(s, s->list_items[root.first + k], 0);
+    need = nk > need ? nk : need;
+  }
+
+  // geometry: LDS-resident when it fits next to the stack (gfx950: 160 KiB per CU)
+  const size_t scene_bytes = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
+  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * sizeof(uint32_t);
+  d->book1_lds = env_flag("RT_BOOK1_LDS", true) && scene_bytes + stack_bytes <= 64 * 1024;
+  d->b1_lds_bytes = (d->book1_lds ? scene_bytes : 0) + stack_bytes;
+
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, d->device));
+  int per_cu = 0;
+  if (d->book1_lds)
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_book1_kernel<true>, b1::kBlock, d->b1_lds_bytes));
+  else
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_book1_kernel<false>, b1::kBlock, d->b1_lds_bytes));
+  if (per_cu < 1) per_cu = 1;
+  d->b1_grid = prop.multiProcessorCount * per_cu;
+  const int spill_lanes = d->b1_grid * b1::kBlock;
+  const size_t spill_bytes = (size_t)(kMaxDepth - b1::kRecRegs) * spill_lanes * sizeof(uint16_t);
+
+  size_t off[6], total = 0;
+  const size_t sizes[6] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+                           roots.size() * sizeof(uint16_t), 256, spill_bytes};
+  for (int k = 0; k < 6; k++) {
+    off[k] = total;
+    total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
+  }
+  void *arena = nullptr;
+  HIP_OK(hipMalloc(&arena, total));
+  char *b = (char *)arena;
+  if (sizes[0]) HIP_OK(hipMemcpy(b + off[0], nodes.data(), sizes[0], hipMemcpyHostToDevice));
+  if (sizes[1]) HIP_OK(hipMemcpy(b + off[1], sph.data(), sizes[1], hipMemcpyHostToDevice));
+  if (sizes[2]) HIP_OK(hipMemcpy(b + off[2], mats.data(), sizes[2], hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b + off[3], roots.data(), sizes[3], hipMemcpyHostToDevice));
+  d->b1_arena = arena;
+  b1::Book1View &V = d->b1view;
+  V.S = d->view;
+  V.nodes_g = (const float4 *)(b + off[0]);
+  V.spheres_g = (const float4 *)(b + off[1]);
+  V.mats = (const b1::FastMat *)(b + off[2]);
+  V.root_items = (const uint16_t *)(b + off[3]);
+  V.work_counter = (int32_t *)(b + off[4]);
+  V.spill = (uint16_t *)(b + off[5]);
+  V.spill_lanes = spill_lanes;
+  V.n_nodes = s->n_bvh;
+  V.n_spheres = s->n_spheres;
+  V.n_root = root.count;
+  V.stack_need = need;
+  d->book1 = true;
+  return 0;
+}
+
 extern "C" int rt_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
 }
+
+extern "C" void rt_scene_release(rt_device_scene *d);
 
 extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) {
   if (s == NULL) {
@@ -225,6 +391,10 @@ extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) 
   const void *dev_arrays[13];
   for (int k = 0; k < 13; k++) dev_arrays[k] = (char *)arena + parts[k].off;
   d->view = make_view(*s, dev_arrays);
+  if (book1_eligible(s) && book1_upload(d, s) != 0) {
+    rt_scene_release(d);
+    return NULL;
+  }
   return d;
 }
 
@@ -232,6 +402,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (!d) return;
   (void)hipSetDevice(d->device);
   (void)hipFree(d->arena);
+  if (d->b1_arena) (void)hipFree(d->b1_arena);
   delete d;
 }
 
@@ -245,6 +416,21 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
   const int64_t npix = (int64_t)n_rows * d->width;
   const dim3 grid((unsigned)((npix + kBlock - 1) / kBlock)), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
+  if (d->book1) {
+    if (npix >= (int64_t)1 << 31) return rt_set_error("too many pixels for one launch"), -1;
+    b1::Book1View V = d->b1view;
+    V.row0 = row0;
+    V.row_stride = row_stride;
+    V.n_rows = n_rows;
+    HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+    const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
+    if (d->book1_lds)
+      hipLaunchKernelGGL(rt_book1_kernel<true>, g1, blk, d->b1_lds_bytes, st, V, d_out);
+    else
+      hipLaunchKernelGGL(rt_book1_kernel<false>, g1, blk, d->b1_lds_bytes, st, V, d_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+  }
   if ((d->features & ~kFeatBook1) == 0)
     hipLaunchKernelGGL(rt_render_rows_kernel<kFeatBook1>, grid, block, 0, st, d->view, row0, row_stride, n_rows, d_out);
   else

@@ -137,3 +137,21 @@ def test_cli_rt_main_matches_golden(manifest, tmp_path):
     e = manifest["renders"]["s0_400x225_10spp_d10"]
     assert hashlib.sha256(data[168:]).hexdigest() == e["sha256"]
     assert data[:168] == open(os.path.join(ROOT, "tests", "golden", "tiff_header.bin"), "rb").read()
+
+
+@pytest.mark.parametrize("env", [{"RT_BOOK1": "0"}, {"RT_BOOK1_LDS": "0"}, {}])
+@pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
+def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
+    """Book-1 scenes run on the persistent fast kernel (LDS or global geometry) unless RT_BOOK1=0
+    selects the general kernel; every variant must reproduce the reference frame."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = manifest["renders"][name]
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    _check(img, golden_image(e), f"{name} {env}")
+
+
+def test_book1_deep_paths_spill(monkeypatch):
+    """max_depth 64 with a glass-heavy view: paths longer than the register record spill to HBM."""
+    sc = rtc.Scene.preset(1, 160, 24, 64)
+    _check(rtc.render(sc), pyoracle.render(sc), "scene 1 depth 64")
