@@ -58,7 +58,8 @@ int rt_render(const rt_flat_scene *scene, int n_gpus, uint8_t *out_host);
 double rt_last_kernel_ms(int device);
 
 /* Diagnostics: evaluate the device libm port (rt_libm.h) on n inputs.
- * fn: 0 = sincosf (out[2i] = sin, out[2i+1] = cos), 1 = powf(x, 5), 2 = logf, 3 = sinf. */
+ * fn: 0 = sincosf (out[2i] = sin, out[2i+1] = cos), 1 = powf(x, 5), 2 = logf, 3 = sinf,
+ *     4 = atan2f(x[2i], x[2i+1]) into out[i] (n = 2 * pairs), 5 = acosf. */
 int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device);
 
 const char *rt_last_error(void);

@@ -367,8 +367,8 @@ RT_D void make_record(const DScene &S, f3 wo, f3 wd, const Hit &h, Rec &r) {
     r.front = dot(d, outward) < 0.0f;
     r.normal = r.front ? outward : neg(outward);
     if (F & RT_FEAT_TEX_UV) {
-      r.u = (atan2f(-outward.z, outward.x) + kPi) * kInvPi * 0.5f;
-      r.v = acosf(-outward.y) * kInvPi;
+      r.u = (rtm::atan2f(-outward.z, outward.x) + kPi) * kInvPi * 0.5f;  // glibc-exact ports
+      r.v = rtm::acosf(-outward.y) * kInvPi;
     }
     r.material = s.material;
   } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {

@@ -79,8 +79,12 @@ __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t 
     out[k] = rtm::powf(v, 5.0f);
   } else if (fn == 2) {
     out[k] = rtm::logf(v);
-  } else {
+  } else if (fn == 3) {
     out[k] = rtm::sinf(v);
+  } else if (fn == 4) {  // atan2f(y = x[2k], x = x[2k+1]) for k < n/2
+    if (2 * k + 1 < n) out[k] = rtm::atan2f(v, x[2 * k + 1]);
+  } else {
+    out[k] = rtm::acosf(v);
   }
 }
 

@@ -12,6 +12,8 @@
 //   powf     src/material.c:73      (Dielectric Schlick term, y = 5)
 //   logf     src/hittable.c:413     (ConstantMedium free-flight distance)
 //   sinf     src/texture.c:50       (Perlin marble)
+//   atan2f   src/hittable.c:146     (sphere u; glibc 2.35 e_atan2f.c + s_atanf.c, fdlibm)
+//   acosf    src/hittable.c:147     (sphere v; glibc 2.35 e_acosf.c, fdlibm)
 //
 // Algorithm + tables: glibc sysdeps/ieee754/flt-32/{s_sincosf.c,sincosf.h,e_powf.c,e_logf.c,
 // s_sinf.c} (ARM optimized-routines).  The FMA placement below is the one gcc emitted for the
@@ -302,6 +304,132 @@ RT_HD float logf(float x) {
   y = fmad(-0x1.00ea348b88334p-2, r2, y);
   y = fmad(y, r2, y0 + r);
   return (float)y;
+}
+
+// ---------------------------------------------------------------- atanf / atan2f / acosf
+// fdlibm single precision as in glibc 2.35 sysdeps/ieee754/flt-32 (no multiarch variant: plain
+// SSE float arithmetic).  Constants read from /lib/x86_64-linux-gnu/libm.so.6.
+RT_HD float atanf(float x) {
+  const float atanhi[4] = {u2f(0x3eed6338), u2f(0x3f490fda), u2f(0x3f7b985e), u2f(0x3fc90fda)};
+  const float atanlo[4] = {u2f(0x31ac3769), u2f(0x33222168), u2f(0x33140fb4), u2f(0x33a22168)};
+  const uint32_t hx = f2u(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c000000) {  // |x| >= 2^25
+    if (ix > 0x7f800000) return x + x;
+    return ((int32_t)hx > 0) ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3ee00000) {              // |x| < 0.4375
+    if (ix < 0x31000000) return x;    // |x| < 2^-29
+    id = -1;
+  } else {
+    x = fabsf(x);
+    if (ix < 0x3f980000) {            // |x| < 1.1875
+      if (ix < 0x3f300000) {          // 7/16 <= |x| < 11/16
+        id = 0;
+        x = (2.0f * x - 1.0f) / (2.0f + x);
+      } else {                        // 11/16 <= |x| < 19/16
+        id = 1;
+        x = (x - 1.0f) / (x + 1.0f);
+      }
+    } else if (ix < 0x401c0000) {     // |x| < 2.4375
+      id = 2;
+      x = (x - 1.5f) / (1.0f + 1.5f * x);
+    } else {                          // 2.4375 <= |x| < 2^25
+      id = 3;
+      x = -1.0f / x;
+    }
+  }
+  const float z = x * x;
+  const float w = z * z;
+  // Horner exactly as fdlibm writes it: s1 = z*(aT0+w*(aT2+w*(aT4+w*(aT6+w*(aT8+w*aT10)))))
+  const float t1 = z * (u2f(0x3eaaaaab) +
+                        w * (u2f(0x3e124925) +
+                             w * (u2f(0x3dba2e6e) + w * (u2f(0x3d886b35) + w * (u2f(0x3d4bda59) + w * u2f(0x3c8569d7))))));
+  // s2 = w*(aT1+w*(aT3+w*(aT5+w*(aT7+w*aT9))))
+  const float t2 = w * (u2f(0xbe4ccccd) +
+                        w * (u2f(0xbde38e38) + w * (u2f(0xbd9d8795) + w * (u2f(0xbd6ef16b) + w * u2f(0xbd15a221)))));
+  if (id < 0) return x - x * (t1 + t2);
+  const float r = atanhi[id] - ((x * (t1 + t2) - atanlo[id]) - x);
+  return ((int32_t)hx < 0) ? -r : r;
+}
+
+RT_HD float atan2f(float y, float x) {
+  const float tiny = 1.0e-30f, pi_o_4 = u2f(0x3f490fdb), pi_o_2 = u2f(0x3fc90fdb), pi = u2f(0x40490fdb);
+  const float pi_lo = u2f(0xb3bbbd2e);
+  const uint32_t hx = f2u(x), hy = f2u(y);
+  const uint32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return atanf(y);
+  const int m = (int)(((hy >> 31) & 1) | ((hx >> 30) & 2));
+  if (iy == 0) {
+    if (m <= 1) return y;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if (ix == 0) return ((int32_t)hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      switch (m) {
+      case 0: return pi_o_4 + tiny;
+      case 1: return -pi_o_4 - tiny;
+      case 2: return 3.0f * pi_o_4 + tiny;
+      default: return -3.0f * pi_o_4 - tiny;
+      }
+    }
+    switch (m) {
+    case 0: return 0.0f;
+    case 1: return -0.0f;
+    case 2: return pi + tiny;
+    default: return -pi - tiny;
+    }
+  }
+  if (iy == 0x7f800000) return ((int32_t)hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int32_t k = ((int32_t)iy - (int32_t)ix) >> 23;
+  float z;
+  if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+  else if ((int32_t)hx < 0 && k < -60) z = 0.0f;
+  else z = atanf(fabsf(y / x));
+  switch (m) {
+  case 0: return z;
+  case 1: return u2f(f2u(z) ^ 0x80000000u);
+  case 2: return pi - (z - pi_lo);
+  default: return (z - pi_lo) - pi;
+  }
+}
+
+RT_HD float acosf(float x) {
+  const float pi = u2f(0x40490fda), pio2_hi = u2f(0x3fc90fda), pio2_lo = u2f(0x33a22168);
+  const float pS0 = u2f(0x3e2aaaab), pS1 = u2f(0xbea6b090), pS2 = u2f(0x3e4e0aa8), pS3 = u2f(0xbd241146),
+              pS4 = u2f(0x3a4f7f04), pS5 = u2f(0x3811ef08);
+  const float qS1 = u2f(0xc019d139), qS2 = u2f(0x4001572d), qS3 = u2f(0xbf303361), qS4 = u2f(0x3d9dc62e);
+  const uint32_t hx = f2u(x), ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) return ((int32_t)hx > 0) ? 0.0f : pi + 2.0f * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {  // |x| < 0.5
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+    const float z = x * x;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if ((int32_t)hx < 0) {  // x < -0.5
+    const float z = (1.0f + x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = sqrtf(z);
+    const float r = p / q;
+    const float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  }
+  const float z = (1.0f - x) * 0.5f;  // x > 0.5
+  const float s = sqrtf(z);
+  const float df = u2f(f2u(s) & 0xfffff000u);
+  const float c = (z - df * df) / (s + df);
+  const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  const float r = p / q;
+  const float w = r * s + c;
+  return 2.0f * (df + w);
 }
 
 }  // namespace rtm

@@ -227,10 +227,11 @@ def assemble_frame(parts, height: int, world: int) -> np.ndarray:
 
 
 def diag_libm(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:
-    """Evaluate the device libm port (0 sincosf, 1 powf(x,5), 2 logf, 3 sinf) on float32 inputs."""
+    """Evaluate the device libm port on float32 inputs: 0 sincosf, 1 powf(x,5), 2 logf, 3 sinf,
+    4 atan2f over interleaved (y, x) pairs, 5 acosf."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     out = np.empty(2 * x.size if fn == 0 else x.size, dtype=np.float32)
     rc = lib().rt_diag_libm(int(fn), x.ctypes.data, out.ctypes.data, x.size, int(device))
     if rc != 0:
         raise RtcError(f"rt_diag_libm failed: {last_error()}")
-    return out
+    return out[: x.size // 2] if fn == 4 else out

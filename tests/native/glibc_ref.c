@@ -9,3 +9,5 @@ void ref_sincosf(const float *x, float *out, int64_t n) {
 void ref_pow5(const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = powf(x[i], 5.0f); }
 void ref_logf(const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = logf(x[i]); }
 void ref_sinf(const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = sinf(x[i]); }
+void ref_atan2f(const float *yx, float *out, int64_t n_pairs) { for (int64_t i = 0; i < n_pairs; i++) out[i] = atan2f(yx[2 * i], yx[2 * i + 1]); }
+void ref_acosf(const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = acosf(x[i]); }

@@ -24,6 +24,10 @@ int main(int argc, char **argv) {
   else if (!strcmp(fn, "pow5")) { mode = 2; lo = 0; hi = 0x40000001ull; }
   else if (!strcmp(fn, "logf_f32")) { mode = 3; lo = 1; hi = 1ull << 24; }
   else if (!strcmp(fn, "logf_all")) { mode = 4; lo = 0; hi = 0x80000000ull; }
+  else if (!strcmp(fn, "atanf_all")) { mode = 5; lo = 0; hi = 1ull << 32; }
+  else if (!strcmp(fn, "acosf_unit")) { mode = 6; lo = 0; hi = 1ull << 32; }
+  else if (!strcmp(fn, "atan2f_rand")) { mode = 7; lo = 0; hi = 1ull << 28; }
+  else if (!strcmp(fn, "uv_sphere")) { mode = 8; lo = 0; hi = 1ull << 26; }
   else { fprintf(stderr, "unknown fn\n"); return 2; }
   if (argc >= 4) { lo = strtoull(argv[2], 0, 0); hi = strtoull(argv[3], 0, 0); }
   const int nt = omp_get_max_threads();
@@ -53,6 +57,32 @@ int main(int argc, char **argv) {
         break;
       case 2:
         x = rtm::u2f((uint32_t)k); r0 = powf(x, 5.0f); p0 = rtm::powf(x, 5.0f);
+        h = fnv_mix(h, rtm::f2u(r0));
+        if (rtm::f2u(r0) != rtm::f2u(p0) && !(isnan(r0) && isnan(p0))) { nb++;
+#pragma omp critical
+          if (first_bad < 0) first_bad = (long long)k; }
+        break;
+      case 5: x = rtm::u2f((uint32_t)k); r0 = atanf(x); p0 = rtm::atanf(x); goto cmp1;
+      case 6: x = rtm::u2f((uint32_t)k); if (!(fabsf(x) <= 1.0f)) continue; r0 = acosf(x); p0 = rtm::acosf(x); goto cmp1;
+      case 7: {  // random (y, x) pairs over all finite floats, plus a dense [-1,1]^2 half
+        uint64_t z = k * 0x9e3779b97f4a7c15ULL; z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
+        float y = rtm::u2f((uint32_t)z), xx = rtm::u2f((uint32_t)(z >> 32));
+        if (k & 1) { y = (float)((int32_t)(uint32_t)z) * 0x1p-31f; xx = (float)((int32_t)(uint32_t)(z >> 32)) * 0x1p-31f; }
+        if (isnan(y) || isnan(xx)) continue;
+        r0 = atan2f(y, xx); p0 = rtm::atan2f(y, xx); x = y; goto cmp1; }
+      case 8: {  // u,v of unit normals as Sphere_hit computes them (src/hittable.c:146-147)
+        uint64_t z = k * 0x9e3779b97f4a7c15ULL; z ^= z >> 31; z *= 0x94d049bb133111ebULL; z ^= z >> 29;
+        float a = (float)((uint32_t)z >> 8) * 0x1p-24f * 2.0f - 1.0f, b = (float)((uint32_t)(z >> 32) >> 8) * 0x1p-24f * 2.0f - 1.0f;
+        float c = (float)((uint32_t)(z >> 16) >> 8) * 0x1p-24f * 2.0f - 1.0f;
+        float inv = 1.0f / sqrtf((a * a + b * b) + c * c); a *= inv; b *= inv; c *= inv;
+        r0 = atan2f(-c, a); p0 = rtm::atan2f(-c, a);
+        r1 = acosf(-b); p1 = rtm::acosf(-b);
+        h = fnv_mix(fnv_mix(h, rtm::f2u(r0)), rtm::f2u(r1));
+        if (rtm::f2u(r0) != rtm::f2u(p0) || rtm::f2u(r1) != rtm::f2u(p1)) { nb++;
+#pragma omp critical
+          if (first_bad < 0) first_bad = (long long)k; }
+        break; }
+      cmp1:
         h = fnv_mix(h, rtm::f2u(r0));
         if (rtm::f2u(r0) != rtm::f2u(p0) && !(isnan(r0) && isnan(p0))) { nb++;
 #pragma omp critical

@@ -5,6 +5,8 @@ CPU: the port compiled for the host (hipcc host pass), exhaustively:
   sincosf on all 2^24 Lambertian/Sphere_rand angles phi = (2*(float)pi) * k/2^24
   powf(x, 5) on every float in [0, 2]            (Dielectric Schlick term, src/material.c:73)
   logf on all 2^24 pcg32_f32 values              (ConstantMedium, src/hittable.c:413)
+  atanf on every float, acosf on every float in [-1, 1], atan2f on 2^28 random pairs and the
+  sphere u,v expression on 2^26 unit normals   (Sphere_hit u,v, src/hittable.c:146-147)
 GPU: the same functions compiled for gfx950, on the same domains (pow5 strided), through the
 C ABI's rt_diag_libm, compared with glibc evaluated on the host.
 """
@@ -21,7 +23,8 @@ from conftest import ROOT
 BIN = os.path.join(ROOT, "tests", "native", "bin")
 
 
-@pytest.mark.parametrize("fn", ["sincos_phi", "pow5", "logf_f32"])
+@pytest.mark.parametrize("fn", ["sincos_phi", "pow5", "logf_f32", "atanf_all", "acosf_unit", "atan2f_rand",
+                                "uv_sphere"])
 def test_port_exhaustive_on_host(fn):
     r = subprocess.run([os.path.join(BIN, "libm_check"), fn], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and " mismatches=0 " in r.stdout, r.stdout + r.stderr
@@ -37,7 +40,7 @@ def test_port_sincos_large_arguments_sample_on_host():
 
 def _glibc():
     L = ctypes.CDLL(os.path.join(BIN, "libglibc_ref.so"))
-    for n in ("ref_sincosf", "ref_pow5", "ref_logf", "ref_sinf"):
+    for n in ("ref_sincosf", "ref_pow5", "ref_logf", "ref_sinf", "ref_atan2f", "ref_acosf"):
         getattr(L, n).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         getattr(L, n).restype = None
     return L
@@ -90,3 +93,18 @@ def test_device_sinf_random_and_special():
     x = np.concatenate([x, specials]).astype(np.float32)
     ok = _same_bits(rtc.diag_libm(3, x), _host("ref_sinf", x, x.size))
     assert ok.all(), f"{(~ok).sum()} mismatches, first x={x[np.argmin(ok)]!r}"
+
+
+@pytest.mark.gpu
+def test_device_atan2f_acosf_sphere_uv():
+    """u, v of the sphere hit record (Checker / Image textures) on the device, vs glibc."""
+    rng = np.random.default_rng(3)
+    v = rng.normal(size=(1 << 22, 3)).astype(np.float32)
+    v /= np.sqrt((v * v).sum(axis=1, keepdims=True)).astype(np.float32)
+    yx = np.stack([-v[:, 2], v[:, 0]], axis=1).astype(np.float32).ravel()
+    ok = _same_bits(rtc.diag_libm(4, yx), _host("ref_atan2f", yx, yx.size // 2))
+    assert ok.all(), f"atan2f: {(~ok).sum()} mismatches"
+    a = np.concatenate([-v[:, 1], rng.uniform(-1, 1, 1 << 20).astype(np.float32),
+                        np.array([-1.0, 1.0, 0.0, -0.0, 0.5, -0.5], np.float32)])
+    ok = _same_bits(rtc.diag_libm(5, a), _host("ref_acosf", a, a.size))
+    assert ok.all(), f"acosf: {(~ok).sum()} mismatches"
