@@ -38,7 +38,7 @@ struct FastMat {   // 32 B: material resolved to what the Book-1 path needs
 
 struct Book1View {
   DScene S;                  // full scene (global memory): sphere aux data, camera
-  const float4 *nodes_g;     // 2 float4 per node: (lo.xyz, left as int bits), (hi.xyz, right bits)
+  const float4 *nodes_g;     // 2 float4 per node: (lo.x hi.x lo.y hi.y), (lo.z hi.z left right bits)
   const float4 *spheres_g;   // (center.xyz, r^2)
   const FastMat *mats;
   const uint16_t *root_items;
@@ -46,6 +46,7 @@ struct Book1View {
   int32_t stack_need;
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
+  int32_t shade_batch;       // v3: shade once this many lanes of a wave are waiting
   uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
   int32_t spill_lanes;
 };
@@ -117,9 +118,10 @@ RT_D void trace(const Book1View &V, const float4 *nodes, const float4 *sph, uint
       if (cur & kLeafBit) {
         sphere_test_lds(sph, (int)(cur & 0x7fff), T, tmin);
       } else {
-        const float4 lo = nodes[2 * cur], hi = nodes[2 * cur + 1];
+        const float4 na = nodes[2 * cur], nb = nodes[2 * cur + 1];
+        const float4 lo = make_float4(na.x, na.z, nb.x, 0.0f), hi = make_float4(na.y, na.w, nb.y, 0.0f);
         if (aabb_lds(lo, hi, T, tmin)) {
-          const uint32_t l = __float_as_uint(lo.w), r = __float_as_uint(hi.w);
+          const uint32_t l = __float_as_uint(nb.z), r = __float_as_uint(nb.w);
           if (l & kLeafBit) {
             sphere_test_lds(sph, (int)(l & 0x7fff), T, tmin);
             if (r != 0xffffu) {
@@ -343,6 +345,273 @@ __device__ void render(const Book1View &V, uint8_t *__restrict__ out, char *lds)
         need_sample = true;
       }
     }
+  }
+}
+
+
+// quantize one pixel (src/raytracing.c:127-131): mean, gamma 2, clamp-macro semantics, truncate
+RT_D uint8_t quantize(float sum, float spp_f) {
+  float v = sqrtf(sum / spp_f);
+  v = v > 0.0f ? v : 0.0f;
+  v = v < 0.999f ? v : 0.999f;
+  return (uint8_t)(int)(256.0f * v);
+}
+RT_D void write_pixel(uint8_t *dst, f3 acc, int spp) {
+  const float spp_f = (float)spp;
+  dst[0] = quantize(acc.x, spp_f);
+  dst[1] = quantize(acc.y, spp_f);
+  dst[2] = quantize(acc.z, spp_f);
+}
+
+// ================================================================ v3: batched-shading megaloop
+// The v2 loop (render) makes every lane of a wave wait for the wave's longest traversal, then run
+// every material's shading code: PMC showed ~20% of lanes active per VALU instruction.  v3 keeps
+// each lane's traversal state live across iterations and runs, per wave iteration, EITHER
+// kSteps traversal steps for the lanes still traversing OR one shading pass for the lanes whose
+// ray is resolved -- the latter only once at least `shade_batch` lanes are waiting (wave ballot)
+// or nobody is traversing.  Visit order, t_max and arithmetic are exactly v2's (= the reference).
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct Lane {
+  f3 o, d, inv;       // current ray and 1/d (hoisted: same IEEE division as AABB_hit)
+  float a, tmax;      // |d|^2, closest hit so far
+  int32_t hit;        // sphere index or -1
+  uint32_t cur;       // ref being visited (16-bit encoding)
+  int sp, k;          // LDS stack depth, root-list position
+};
+
+// AABB_hit with the slabs evaluated together: t_min / t_max only tighten and fmaxf/fminf ignore a
+// NaN operand, so testing tmax <= tmin once after all three slabs returns exactly what the
+// reference's per-slab early exit returns.  (lo,hi) pairs are packed: one v_pk_add + v_pk_mul per
+// axis.  Swap on a negative 1/d as the reference does (select, not min/max, for NaN parity).
+RT_D bool aabb_packed(float4 a, float4 b, const Lane &L, float tmin) {
+  const f2v tx = (f2v){a.x, a.y} - L.o.x, ty = (f2v){a.z, a.w} - L.o.y, tz = (f2v){b.x, b.y} - L.o.z;
+  const f2v px = tx * L.inv.x, py = ty * L.inv.y, pz = tz * L.inv.z;
+  const float t0x = L.inv.x < 0 ? px.y : px.x, t1x = L.inv.x < 0 ? px.x : px.y;
+  const float t0y = L.inv.y < 0 ? py.y : py.x, t1y = L.inv.y < 0 ? py.x : py.y;
+  const float t0z = L.inv.z < 0 ? pz.y : pz.x, t1z = L.inv.z < 0 ? pz.x : pz.y;
+  const float lo = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);
+  const float hi = fminf(fminf(fminf(L.tmax, t1x), t1y), t1z);
+  return !(hi <= lo);
+}
+
+RT_D void sphere_test_lane(const float4 *sph, uint32_t ref, Lane &L, float tmin) {
+  const int idx = (int)(ref & 0x7fff);
+  const float4 s = sph[idx];
+  const f3 oc = sub(L.o, mk(s.x, s.y, s.z));
+  const float b = dot(oc, L.d);
+  const float c = dot(oc, oc) - s.w;
+  const float disc = b * b - L.a * c;
+  if (disc < 0) return;
+  const float sq = sqrtf(disc);
+  float root = (-b - sq) / L.a;
+  if (root <= tmin || root >= L.tmax) {
+    root = (-b + sq) / L.a;
+    if (root <= tmin || root >= L.tmax) return;
+  }
+  L.tmax = root;
+  L.hit = idx;
+}
+
+// One DFS step (node box test, or leaf sphere(s)); returns true when the ray's traversal is done.
+RT_D bool trav_step(const Book1View &V, const float4 *nodes3, const float4 *sph, uint16_t *stack, Lane &L,
+                    float tmin) {
+  uint32_t t0 = 0xffffu, t1 = 0xffffu;  // spheres to test in this step, in visit order
+  bool moved = false;
+  if (L.cur & kLeafBit) {
+    t0 = L.cur;
+  } else {
+    const float4 a = nodes3[2 * L.cur], b = nodes3[2 * L.cur + 1];
+    if (aabb_packed(a, b, L, tmin)) {
+      const uint32_t l = __float_as_uint(b.z), r = __float_as_uint(b.w);
+      if (l & kLeafBit) {
+        t0 = l;
+        if (r & kLeafBit) {
+          if (r != 0xffffu) t1 = r;
+        } else {
+          L.cur = r;
+          moved = true;
+        }
+      } else {
+        if (r != 0xffffu) {
+          stack[L.sp * kBlock] = (uint16_t)r;
+          L.sp++;
+        }
+        L.cur = l;
+        moved = true;
+      }
+    }
+  }
+  if (t0 != 0xffffu) sphere_test_lane(sph, t0, L, tmin);
+  if (t1 != 0xffffu) sphere_test_lane(sph, t1, L, tmin);
+  if (moved) return false;
+  if (L.sp > 0) {
+    L.sp--;
+    L.cur = stack[L.sp * kBlock];
+    return false;
+  }
+  if (++L.k < V.n_root) {
+    L.cur = V.root_items[L.k];
+    return false;
+  }
+  return true;
+}
+
+enum : int { kTrav = 0, kWait = 1, kExit = 2 };
+constexpr int kSteps = 4;
+
+template <bool kLds>
+__device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
+  const int tid = threadIdx.x;
+  const int W = V.S.cam.width;
+  const int64_t total = (int64_t)V.n_rows * W;
+  // LDS: nodes (lo.x hi.x lo.y hi.y | lo.z hi.z left right) + spheres, then the 16-bit stacks
+  float4 *nodes3 = (float4 *)lds;
+  float4 *sph = nodes3 + (kLds ? 2 * V.n_nodes : 0);
+  uint16_t *stack_base = (uint16_t *)(sph + (kLds ? V.n_spheres : 0));
+  if (kLds) {
+    for (int q = tid; q < 2 * V.n_nodes; q += kBlock) nodes3[q] = V.nodes_g[q];
+    for (int q = tid; q < V.n_spheres; q += kBlock) sph[q] = V.spheres_g[q];
+    __syncthreads();
+  } else {
+    nodes3 = (float4 *)V.nodes_g;
+    sph = (float4 *)V.spheres_g;
+  }
+  uint16_t *stack = stack_base + tid;
+  const int glane = blockIdx.x * kBlock + tid;
+  const int lane = lane_id();
+  const rt_camera &cam = V.S.cam;
+  const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
+  const bool dof = cam.dof_angle > 0.0f;
+  const int spp = cam.spp, max_depth = cam.max_depth;
+  const float tmin = 1e-3f;
+
+  int mode = kWait;
+  bool have_result = false;  // false: this lane first needs a pixel
+  int64_t pix = 0;
+  int i = 0, j = 0, s = 0, depth = 0;
+  Pcg32 g;
+  g.state = 0;
+  g.inc = 0;
+  f3 acc = mk(0, 0, 0);
+  Record R;
+  R.r0 = R.r1 = 0;
+  R.n = 0;
+  Lane L;
+  L.o = L.d = L.inv = mk(0, 0, 0);
+  L.a = L.tmax = 0.0f;
+  L.hit = -1;
+  L.cur = 0;
+  L.sp = L.k = 0;
+
+  for (;;) {
+    const uint64_t trav = __ballot(mode == kTrav);
+    const uint64_t wait = __ballot(mode == kWait);
+    if ((trav | wait) == 0) break;
+    if (trav != 0 && (int)__popcll(wait) < V.shade_batch) {
+      // ---------------- traversal steps for every lane still traversing
+      if (mode == kTrav) {
+#pragma unroll
+        for (int u = 0; u < kSteps; u++)
+          if (mode == kTrav && trav_step(V, nodes3, sph, stack, L, tmin)) mode = kWait;
+      }
+      continue;
+    }
+    if (mode != kWait) continue;
+    // ---------------- shading pass (Camera_ray_color body after hit(), src/raytracing.c:44-75)
+    bool need_pixel = !have_result, need_sample = false;
+    if (have_result) {
+      bool path_done;
+      f3 tail = mk(0.0f, 0.0f, 0.0f);
+      if (L.hit < 0) {
+        tail = ld3(cam.background);
+        path_done = true;
+      } else {
+        const rt_sphere &sp = V.S.spheres[L.hit];
+        const f3 p = ray_at(L.o, L.d, L.tmax);
+        const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
+        const bool front = dot(L.d, outward) < 0.0f;
+        const f3 normal = front ? outward : neg(outward);
+        const FastMat &m = V.mats[sp.material];
+        const f3 nd = scatter(m, normal, front, L.d, g);
+        rec_push(V, R, (uint32_t)sp.material, glane);
+        L.o = p;
+        L.d = nd;
+        depth--;
+        path_done = depth <= 0;  // the next call would return 0 at depth 0 (src/raytracing.c:40)
+      }
+      if (path_done) {
+        acc = add(acc, rec_fold(V, R, tail, glane));
+        s++;
+        if (s == spp) {  // quantize (src/raytracing.c:127-131)
+          write_pixel(out + pix * 3, acc, spp);
+          need_pixel = true;
+        } else {
+          need_sample = true;
+        }
+      }
+    }
+    while (need_pixel || need_sample) {
+      if (need_pixel) {  // work stealing among the lanes that need a pixel right now
+        const uint64_t want = __ballot(true);
+        const int first = __builtin_ctzll(want);
+        int base = 0;
+        if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
+        base = __shfl(base, first);
+        pix = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
+        if (pix >= total) {
+          mode = kExit;
+          break;
+        }
+        const int jj = (int)(pix / W);
+        i = (int)(pix - (int64_t)jj * W);
+        j = V.row0 + jj * V.row_stride;
+        g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
+        acc = mk(0.0f, 0.0f, 0.0f);
+        s = 0;
+        need_pixel = false;
+      }
+      // camera ray (src/raytracing.c:96-122)
+      const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+      const float px = g.between(-0.5f, 0.5f);
+      const float py = g.between(-0.5f, 0.5f);
+      f3 o = lf;
+      if (dof) {
+        float a, b;
+        for (;;) {
+          a = g.between(-1.0f, 1.0f);
+          b = g.between(-1.0f, 1.0f);
+          if (a * a + b * b < 1.0f) break;
+        }
+        o = add(add(lf, scale(ld3(cam.disc_u), a)), scale(ld3(cam.disc_v), b));
+      }
+      L.o = o;
+      L.d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+      depth = max_depth;
+      R.n = 0;
+      need_sample = false;
+      if (depth <= 0) {  // Camera_ray_color returns 0 without tracing
+        acc = add(acc, mk(0.0f, 0.0f, 0.0f));
+        s++;
+        if (s == spp) {
+          write_pixel(out + pix * 3, acc, spp);
+          need_pixel = true;
+        } else {
+          need_sample = true;
+        }
+      }
+    }
+    if (mode == kExit) continue;
+    // set up the traversal of the new ray
+    L.inv = mk(1.0f / L.d.x, 1.0f / L.d.y, 1.0f / L.d.z);
+    L.a = dot(L.d, L.d);
+    L.tmax = __builtin_inff();
+    L.hit = -1;
+    L.sp = 0;
+    L.k = 0;
+    L.cur = V.root_items[0];
+    have_result = true;
+    mode = V.n_root > 0 ? kTrav : kWait;
   }
 }
 

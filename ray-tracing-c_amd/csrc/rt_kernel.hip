@@ -60,10 +60,13 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
 }
 
 // Persistent Book-1 kernel (rt_book1.h): grid = resident workgroups, lanes steal pixels.
-template <bool kLds>
+template <bool kLds, int kVer>
 __global__ __launch_bounds__(b1::kBlock) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  b1::render<kLds>(V, out, lds);
+  if (kVer == 3)
+    b1::render_batched<kLds>(V, out, lds);
+  else
+    b1::render<kLds>(V, out, lds);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -82,7 +85,7 @@ __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t 
   } else if (fn == 3) {
     out[k] = rtm::sinf(v);
   } else if (fn == 4) {  // atan2f(y = x[2k], x = x[2k+1]) for k < n/2
-    if (2 * k + 1 < n) out[k] = rtm::atan2f(v, x[2 * k + 1]);
+    if (2 * k + 1 < n) out[k] = rtm::atan2f(x[2 * k], x[2 * k + 1]);
   } else {
     out[k] = rtm::acosf(v);
   }
@@ -99,6 +102,7 @@ struct rt_device_scene {
   // Book-1 fast path (rt_book1.h), when the scene qualifies
   bool book1 = false;
   bool book1_lds = false;
+  int book1_ver = 3;
   b1::Book1View b1view;
   void *b1_arena = nullptr;
   int b1_grid = 0;
@@ -252,8 +256,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     uint32_t l, r;
     pack_ref(n.left, &l);
     pack_ref(n.right, &r);
-    nodes[2 * k] = make_float4(n.lo[0], n.lo[1], n.lo[2], bits_as_float(l));
-    nodes[2 * k + 1] = make_float4(n.hi[0], n.hi[1], n.hi[2], bits_as_float(r));
+    nodes[2 * k] = make_float4(n.lo[0], n.hi[0], n.lo[1], n.hi[1]);  // the reference's AABB values[axis][lo/hi]
+    nodes[2 * k + 1] = make_float4(n.lo[2], n.hi[2], bits_as_float(l), bits_as_float(r));
   }
   std::vector<float4> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++)
@@ -288,17 +292,21 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
 
   // geometry: LDS-resident when it fits next to the stack (gfx950: 160 KiB per CU)
   const size_t scene_bytes = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
-  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * sizeof(uint32_t);
+  {
+    const char *ev = getenv("RT_BOOK1_V");
+    d->book1_ver = (ev && *ev == '2') ? 2 : 3;
+  }
+  // v2 keeps 32-bit stack slots, v3 16-bit ones
+  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * (d->book1_ver == 3 ? 2 : 4);
   d->book1_lds = env_flag("RT_BOOK1_LDS", true) && scene_bytes + stack_bytes <= 64 * 1024;
-  d->b1_lds_bytes = (d->book1_lds ? scene_bytes : 0) + stack_bytes;
+  d->b1_lds_bytes = align_up((d->book1_lds ? scene_bytes : 0) + stack_bytes, 16);
 
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0;
-  if (d->book1_lds)
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_book1_kernel<true>, b1::kBlock, d->b1_lds_bytes));
-  else
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_book1_kernel<false>, b1::kBlock, d->b1_lds_bytes));
+  const void *fn = d->book1_ver == 3 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 3> : (const void *)rt_book1_kernel<false, 3>)
+                                      : (d->book1_lds ? (const void *)rt_book1_kernel<true, 2> : (const void *)rt_book1_kernel<false, 2>);
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, b1::kBlock, d->b1_lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->b1_grid = prop.multiProcessorCount * per_cu;
   const int spill_lanes = d->b1_grid * b1::kBlock;
@@ -332,6 +340,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.n_spheres = s->n_spheres;
   V.n_root = root.count;
   V.stack_need = need;
+  {
+    const char *eb = getenv("RT_SHADE_BATCH");
+    V.shade_batch = (eb && *eb) ? atoi(eb) : 32;
+    V.shade_batch = V.shade_batch < 1 ? 1 : (V.shade_batch > 64 ? 64 : V.shade_batch);  // >= 1: progress
+  }
   d->book1 = true;
   return 0;
 }
@@ -428,10 +441,17 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     V.n_rows = n_rows;
     HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
     const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-    if (d->book1_lds)
-      hipLaunchKernelGGL(rt_book1_kernel<true>, g1, blk, d->b1_lds_bytes, st, V, d_out);
-    else
-      hipLaunchKernelGGL(rt_book1_kernel<false>, g1, blk, d->b1_lds_bytes, st, V, d_out);
+    if (d->book1_ver == 3) {
+      if (d->book1_lds)
+        hipLaunchKernelGGL((rt_book1_kernel<true, 3>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+      else
+        hipLaunchKernelGGL((rt_book1_kernel<false, 3>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    } else {
+      if (d->book1_lds)
+        hipLaunchKernelGGL((rt_book1_kernel<true, 2>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+      else
+        hipLaunchKernelGGL((rt_book1_kernel<false, 2>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    }
     HIP_OK(hipGetLastError());
     return 0;
   }
