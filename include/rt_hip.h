@@ -62,6 +62,11 @@ double rt_last_kernel_ms(int device);
  *     4 = atan2f(x[2i], x[2i+1]) into out[i] (n = 2 * pairs), 5 = acosf. */
 int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device);
 
+/* Diagnostics: per-lane counters of the last Book-1 launch built with RT_BOOK1_STATS=1 set at
+ * upload time (trav iterations, useful steps, shade iterations, shading lanes, rays, node visits,
+ * leaf visits, idle-in-shade iterations). */
+int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out8);
+
 const char *rt_last_error(void);
 int rt_abi_version(void);
 

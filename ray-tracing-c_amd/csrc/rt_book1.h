@@ -47,6 +47,7 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // v3: shade once this many lanes of a wave are waiting
+  unsigned long long *stats; // diagnostic counters (kStats builds only)
   uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
   int32_t spill_lanes;
 };
@@ -460,7 +461,9 @@ RT_D bool trav_step(const Book1View &V, const float4 *nodes3, const float4 *sph,
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
 constexpr int kSteps = 4;
 
-template <bool kLds>
+// kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
+// accumulated into V.stats with one atomic per lane at exit; never used for timing.
+template <bool kLds, bool kStats = false>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
   const int W = V.S.cam.width;
@@ -488,6 +491,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 
   int mode = kWait;
   bool have_result = false;  // false: this lane first needs a pixel
+  // stats: 0 trav iterations seen, 1 useful trav steps, 2 shade iterations seen, 3 shading lanes,
+  //        4 rays traced, 5 node visits, 6 leaf tests, 7 shade passes where this lane was idle
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t pix = 0;
   int i = 0, j = 0, s = 0, depth = 0;
   Pcg32 g;
@@ -510,12 +516,23 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     if ((trav | wait) == 0) break;
     if (trav != 0 && (int)__popcll(wait) < V.shade_batch) {
       // ---------------- traversal steps for every lane still traversing
+      if (kStats && mode != kExit) st[0] += kSteps;
       if (mode == kTrav) {
 #pragma unroll
         for (int u = 0; u < kSteps; u++)
-          if (mode == kTrav && trav_step(V, nodes3, sph, stack, L, tmin)) mode = kWait;
+          if (mode == kTrav) {
+            if (kStats) {
+              st[1]++;
+              if (L.cur & kLeafBit) st[6]++; else st[5]++;
+            }
+            if (trav_step(V, nodes3, sph, stack, L, tmin)) mode = kWait;
+          }
       }
       continue;
+    }
+    if (kStats && mode != kExit) {
+      st[2]++;
+      if (mode == kWait) st[3]++; else st[7]++;
     }
     if (mode != kWait) continue;
     // ---------------- shading pass (Camera_ray_color body after hit(), src/raytracing.c:44-75)
@@ -611,8 +628,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     L.k = 0;
     L.cur = V.root_items[0];
     have_result = true;
+    if (kStats) st[4]++;
     mode = V.n_root > 0 ? kTrav : kWait;
   }
+  if (kStats)
+    for (int q = 0; q < 8; q++) atomicAdd(&V.stats[q], st[q]);
 }
 
 }  // namespace b1

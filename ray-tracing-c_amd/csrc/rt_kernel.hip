@@ -63,7 +63,9 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
 template <bool kLds, int kVer>
 __global__ __launch_bounds__(b1::kBlock) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (kVer == 3)
+  if (kVer == 4)  // diagnostic: v3 with per-lane counters
+    b1::render_batched<kLds, true>(V, out, lds);
+  else if (kVer == 3)
     b1::render_batched<kLds>(V, out, lds);
   else
     b1::render<kLds>(V, out, lds);
@@ -295,17 +297,20 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   {
     const char *ev = getenv("RT_BOOK1_V");
     d->book1_ver = (ev && *ev == '2') ? 2 : 3;
+    if (env_flag("RT_BOOK1_STATS", false)) d->book1_ver = 4;
   }
   // v2 keeps 32-bit stack slots, v3 16-bit ones
-  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * (d->book1_ver == 3 ? 2 : 4);
+  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
   d->book1_lds = env_flag("RT_BOOK1_LDS", true) && scene_bytes + stack_bytes <= 64 * 1024;
   d->b1_lds_bytes = align_up((d->book1_lds ? scene_bytes : 0) + stack_bytes, 16);
 
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0;
-  const void *fn = d->book1_ver == 3 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 3> : (const void *)rt_book1_kernel<false, 3>)
-                                      : (d->book1_lds ? (const void *)rt_book1_kernel<true, 2> : (const void *)rt_book1_kernel<false, 2>);
+  const void *fn = d->book1_ver == 4   ? (const void *)rt_book1_kernel<true, 4>
+                   : d->book1_ver == 3 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 3> : (const void *)rt_book1_kernel<false, 3>)
+                                       : (d->book1_lds ? (const void *)rt_book1_kernel<true, 2> : (const void *)rt_book1_kernel<false, 2>);
+  if (d->book1_ver == 4) d->book1_lds = true;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, b1::kBlock, d->b1_lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->b1_grid = prop.multiProcessorCount * per_cu;
@@ -314,7 +319,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
 
   size_t off[6], total = 0;
   const size_t sizes[6] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
-                           roots.size() * sizeof(uint16_t), 256, spill_bytes};
+                           roots.size() * sizeof(uint16_t), 256, spill_bytes};  // [4]: counter + 8 stats
   for (int k = 0; k < 6; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
@@ -334,6 +339,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.mats = (const b1::FastMat *)(b + off[2]);
   V.root_items = (const uint16_t *)(b + off[3]);
   V.work_counter = (int32_t *)(b + off[4]);
+  V.stats = (unsigned long long *)(b + off[4] + 64);
   V.spill = (uint16_t *)(b + off[5]);
   V.spill_lanes = spill_lanes;
   V.n_nodes = s->n_bvh;
@@ -439,9 +445,11 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     V.row0 = row0;
     V.row_stride = row_stride;
     V.n_rows = n_rows;
-    HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+    HIP_OK(hipMemsetAsync(V.work_counter, 0, d->book1_ver == 4 ? 256 : sizeof(int32_t), st));
     const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-    if (d->book1_ver == 3) {
+    if (d->book1_ver == 4) {
+      hipLaunchKernelGGL((rt_book1_kernel<true, 4>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    } else if (d->book1_ver == 3) {
       if (d->book1_lds)
         hipLaunchKernelGGL((rt_book1_kernel<true, 3>), g1, blk, d->b1_lds_bytes, st, V, d_out);
       else
@@ -540,6 +548,14 @@ extern "C" int rt_render(const rt_flat_scene *s, int n_gpus, uint8_t *out_host) 
     rt_scene_release(p.scene);
   }
   return rc;
+}
+
+// Diagnostic counters of the last RT_BOOK1_STATS=1 launch on this scene (8 x u64; see rt_book1.h).
+extern "C" int rt_book1_stats(rt_device_scene *d, unsigned long long *out8) {
+  if (!d || !d->book1 || d->book1_ver != 4) return rt_set_error("no stats build active (RT_BOOK1_STATS=1)"), -1;
+  HIP_OK(hipSetDevice(d->device));
+  HIP_OK(hipMemcpy(out8, d->b1view.stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return 0;
 }
 
 extern "C" int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device) {
