@@ -62,10 +62,22 @@ double rt_last_kernel_ms(int device);
  *     4 = atan2f(x[2i], x[2i+1]) into out[i] (n = 2 * pairs), 5 = acosf. */
 int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device);
 
-/* Diagnostics: per-lane counters of the last Book-1 launch built with RT_BOOK1_STATS=1 set at
- * upload time (trav iterations, useful steps, shade iterations, shading lanes, rays, node visits,
- * leaf visits, idle-in-shade iterations). */
-int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out8);
+/* Diagnostics: counters of the last Book-1 launch built with RT_BOOK1_STATS=1 set at upload time
+ * (first n of: trav iterations, useful steps, shade iterations, shading lanes, rays, node visits,
+ * root-leaf steps, idle-in-shade iterations, shader clocks in traversal / shading iterations,
+ * wave-level traversal / shading iterations, v6 wave-level box / sphere phases or v5 fast / fallback sphere tests, v5 wave-level sphere-code
+ * and fallback executions, clock64 / wall_clock64 ticks of the waves' lifetimes, earliest start / latest end,
+ * latest start, first pixel-counter exhaustion (wall_clock64); n <= 22). */
+int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out, int n);
+/* Diagnostics (same stats build): per work item of the last launch, {traversal steps, duration in
+ * wall_clock64 ticks (100 MHz)} as 2 x uint32 each, for the first n_items items. */
+int rt_book1_pixel_cost(rt_device_scene *dscene, uint32_t *out, int64_t n_items);
+
+/* Diagnostics: bitwise checks of the Book-1 kernel's exact arithmetic cores against the compiler's
+ * sqrtf / division on the device (fn 0: sqrt over float bit patterns start..start+count-1,
+ * fn 1: division on `count` hashed pairs, fn 2: the sphere-hit outcome on hashed rays);
+ * *mismatches receives the number of differing results. */
+int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches, int device);
 
 const char *rt_last_error(void);
 int rt_abi_version(void);

@@ -46,8 +46,11 @@ struct Book1View {
   int32_t stack_need;
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
-  int32_t shade_batch;       // v3: shade once this many lanes of a wave are waiting
+  int32_t shade_batch;       // v3+: shade once this many lanes of a wave are waiting
+  int32_t sphere_batch;      // v6: run a sphere phase once this many lanes have a pending sphere
+  int32_t reverse;           // hand out work items last-first
   unsigned long long *stats; // diagnostic counters (kStats builds only)
+  uint32_t *pixel_cost;      // kStats: per work item {traversal steps, wall_clock64 ticks}
   uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
   int32_t spill_lanes;
 };
@@ -373,11 +376,16 @@ RT_D void write_pixel(uint8_t *dst, f3 acc, int spp) {
 // or nobody is traversing.  Visit order, t_max and arithmetic are exactly v2's (= the reference).
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-struct Lane {
-  f3 o, d, inv;       // current ray and 1/d (hoisted: same IEEE division as AABB_hit)
+struct Lane {         // plain scalars: an f3 member here was kept in scratch by the compiler
+  float ox, oy, oz;   // current ray origin
+  float dx, dy, dz;   // direction
+  float ix, iy, iz;   // 1/d (hoisted: same IEEE division as AABB_hit)
   float a, tmax;      // |d|^2, closest hit so far
+  float ra;           // refined reciprocal of a (div_core), hoisted per ray
+  bool fast;          // a in the range where div_core == '/'
   int32_t hit;        // sphere index or -1
-  uint32_t cur;       // ref being visited (16-bit encoding)
+  uint32_t cur;       // ref being visited (16-bit encoding); v6: 0xffff once the DFS is exhausted
+  uint32_t pend0, pend1;  // v6: leaf spheres found by the last box step, tested before the next one
   int sp, k;          // LDS stack depth, root-list position
 };
 
@@ -386,11 +394,12 @@ struct Lane {
 // reference's per-slab early exit returns.  (lo,hi) pairs are packed: one v_pk_add + v_pk_mul per
 // axis.  Swap on a negative 1/d as the reference does (select, not min/max, for NaN parity).
 RT_D bool aabb_packed(float4 a, float4 b, const Lane &L, float tmin) {
-  const f2v tx = (f2v){a.x, a.y} - L.o.x, ty = (f2v){a.z, a.w} - L.o.y, tz = (f2v){b.x, b.y} - L.o.z;
-  const f2v px = tx * L.inv.x, py = ty * L.inv.y, pz = tz * L.inv.z;
-  const float t0x = L.inv.x < 0 ? px.y : px.x, t1x = L.inv.x < 0 ? px.x : px.y;
-  const float t0y = L.inv.y < 0 ? py.y : py.x, t1y = L.inv.y < 0 ? py.x : py.y;
-  const float t0z = L.inv.z < 0 ? pz.y : pz.x, t1z = L.inv.z < 0 ? pz.x : pz.y;
+  const f2v px = (f2v){(a.x - L.ox) * L.ix, (a.y - L.ox) * L.ix};
+  const f2v py = (f2v){(a.z - L.oy) * L.iy, (a.w - L.oy) * L.iy};
+  const f2v pz = (f2v){(b.x - L.oz) * L.iz, (b.y - L.oz) * L.iz};
+  const float t0x = L.ix < 0 ? px.y : px.x, t1x = L.ix < 0 ? px.x : px.y;
+  const float t0y = L.iy < 0 ? py.y : py.x, t1y = L.iy < 0 ? py.x : py.y;
+  const float t0z = L.iz < 0 ? pz.y : pz.x, t1z = L.iz < 0 ? pz.x : pz.y;
   const float lo = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);
   const float hi = fminf(fminf(fminf(L.tmax, t1x), t1y), t1z);
   return !(hi <= lo);
@@ -399,8 +408,8 @@ RT_D bool aabb_packed(float4 a, float4 b, const Lane &L, float tmin) {
 RT_D void sphere_test_lane(const float4 *sph, uint32_t ref, Lane &L, float tmin) {
   const int idx = (int)(ref & 0x7fff);
   const float4 s = sph[idx];
-  const f3 oc = sub(L.o, mk(s.x, s.y, s.z));
-  const float b = dot(oc, L.d);
+  const f3 oc = sub(mk(L.ox, L.oy, L.oz), mk(s.x, s.y, s.z));
+  const float b = dot(oc, mk(L.dx, L.dy, L.dz));
   const float c = dot(oc, oc) - s.w;
   const float disc = b * b - L.a * c;
   if (disc < 0) return;
@@ -412,6 +421,117 @@ RT_D void sphere_test_lane(const float4 *sph, uint32_t ref, Lane &L, float tmin)
   }
   L.tmax = root;
   L.hit = idx;
+}
+
+// ---------------------------------------------------------------- exact fast arithmetic (v5)
+// What sqrtf() and '/' compile to for f32 on gfx950 (denormals on, correctly rounded): a hardware
+// estimate plus a Newton / one-ulp correction core, wrapped in operand scaling for extreme exponents
+// and a special-value fix-up (v_div_scale / v_div_fmas / v_div_fixup, and the 2^-96 rescale + class
+// test of the sqrt).  On the operand ranges below the wrappers are identities, so the bare cores
+// return the same bits; the division's reciprocal refinement depends on the divisor only and is
+// hoisted per ray.  Bitwise equality is checked on the device by rt_diag_arith (all floats for the
+// sqrt, random pairs for the division: tests/test_render_gpu.py).
+constexpr float kDivLo = 0x1p-20f, kDivHi = 0x1p20f;  // divisor range (|d|^2 of a ray)
+constexpr float kNumHi = 0x1p40f;                     // numerator magnitude bound
+constexpr float kSqrtLo = 0x1p-96f;                   // below it the compiler rescales
+
+RT_D float sqrt_core(float x) {  // == sqrtf(x) for x == 0 or kSqrtLo <= x < inf
+  const float r = __builtin_amdgcn_sqrtf(x);
+  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
+  float out = fmaf(-rm, r, x) <= 0.0f ? rm : r;
+  out = fmaf(-rp, r, x) > 0.0f ? rp : out;
+  return out;
+}
+RT_D float recip_core(float a) {  // the divisor half of the '/' sequence
+  const float y = __builtin_amdgcn_rcpf(a);
+  return fmaf(fmaf(-a, y, 1.0f), y, y);
+}
+RT_D float div_core(float x, float a, float ra) {  // == x / a for a in [kDivLo, kDivHi], |x| <= kNumHi
+  const float q0 = x * ra;
+  const float q1 = fmaf(fmaf(-a, q0, x), ra, q0);
+  return fmaf(fmaf(-a, q1, x), ra, q1);
+}
+// For |x| < 2^-40 (zero and denormals included) div_core is not bit-exact, but both it and x / a
+// are below 2^-18 < t_min in magnitude, so the Sphere_hit root test rejects both: the decision and
+// the recorded root (none) are the same.  Only |x| > kNumHi needs the real division.
+
+// Sphere_hit (src/hittable.c:125-150) with the exact cores; lanes outside their ranges (NaN,
+// huge numerators, tiny discriminants, degenerate rays) evaluate the reference expression.
+template <bool kStats = false>
+RT_D void sphere_test_v5(const float4 *sph, uint32_t ref, Lane &L, float tmin, unsigned long long *st = nullptr) {
+  const int idx = (int)(ref & 0x7fff);
+  const float4 s = sph[idx];
+  const f3 oc = sub(mk(L.ox, L.oy, L.oz), mk(s.x, s.y, s.z));
+  const float b = dot(oc, mk(L.dx, L.dy, L.dz));
+  const float c = dot(oc, oc) - s.w;
+  const float disc = b * b - L.a * c;
+  if (disc < 0) return;
+  float sq = sqrt_core(disc);
+  float r1 = div_core(-b - sq, L.a, L.ra), r2 = div_core(-b + sq, L.a, L.ra);
+  // (bitwise, not short-circuit: one straight-line guard instead of nested branches)
+  const bool ok = (int)L.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                  (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+  if (kStats) {
+    st[ok ? 12 : 13]++;
+    if (!ok && __lane_id() == __builtin_ctzll(__ballot(1))) st[15]++;
+  }
+  if (__builtin_expect(!ok, 0)) {
+    sq = sqrtf(disc);
+    r1 = (-b - sq) / L.a;
+    r2 = (-b + sq) / L.a;
+  }
+  // the reference tries root 1, then root 2, each rejected when (root <= t_min || root >= t_max)
+  const bool take1 = !(r1 <= tmin || r1 >= L.tmax), take2 = !(r2 <= tmin || r2 >= L.tmax);
+  if (take1 || take2) {
+    L.tmax = take1 ? r1 : r2;
+    L.hit = idx;
+  }
+}
+
+// One DFS step, v5: the same visit order as trav_step with the control flow reduced to selects --
+// the right child is stored unconditionally into the free stack slot (the depth only advances on a
+// real push; the stack has one spare slot for it) and the pop reads unconditionally.
+template <bool kStats = false>
+RT_D bool trav_step_v5(const Book1View &V, const float4 *nodes3, const float4 *sph, uint16_t *stack, Lane &L,
+                       float tmin, unsigned long long *st = nullptr) {
+  uint32_t t0 = 0xffffu, t1 = 0xffffu;
+  bool moved = false;
+  const uint32_t cur = L.cur;
+  if (__builtin_expect((cur & kLeafBit) != 0, 0)) {  // a sphere directly in the root list
+    t0 = cur;
+  } else {
+    const float4 a = nodes3[2 * cur], b = nodes3[2 * cur + 1];
+    const bool hit = aabb_packed(a, b, L, tmin);
+    const uint32_t l = __float_as_uint(b.z), r = __float_as_uint(b.w);
+    const bool lleaf = (l & kLeafBit) != 0, rleaf = (r & kLeafBit) != 0;  // kNone has the leaf bit
+    t0 = hit && lleaf ? l : 0xffffu;
+    t1 = hit && lleaf && rleaf ? r : 0xffffu;
+    moved = hit && !(lleaf && rleaf);
+    stack[L.sp * kBlock] = (uint16_t)r;
+    L.sp += (hit && !lleaf && r != 0xffffu) ? 1 : 0;
+    L.cur = moved ? (lleaf ? r : l) : cur;
+  }
+  if (t0 != 0xffffu) {
+    if (kStats && __lane_id() == __builtin_ctzll(__ballot(1))) st[14]++;
+    sphere_test_v5<kStats>(sph, t0, L, tmin, st);
+  }
+  if (t1 != 0xffffu) {
+    if (kStats && __lane_id() == __builtin_ctzll(__ballot(1))) st[14]++;
+    sphere_test_v5<kStats>(sph, t1, L, tmin, st);
+  }
+  if (moved) return false;
+  const int top = L.sp - 1;
+  const uint32_t popped = stack[(top > 0 ? top : 0) * kBlock];
+  if (top >= 0) {
+    L.sp = top;
+    L.cur = popped;
+    return false;
+  }
+  if (++L.k < V.n_root) {
+    L.cur = V.root_items[L.k];
+    return false;
+  }
+  return true;
 }
 
 // One DFS step (node box test, or leaf sphere(s)); returns true when the ray's traversal is done.
@@ -458,12 +578,63 @@ RT_D bool trav_step(const Book1View &V, const float4 *nodes3, const float4 *sph,
   return true;
 }
 
+// ---------------------------------------------------------------- v6: box and sphere phases
+// v5 tests the leaf spheres of a node inside the node's step, so every wave step runs the box code
+// AND two sphere tests whenever any lane of the wave has a leaf -- with a few lanes active in the
+// sphere code.  v6 parks the leaf spheres of a box step in the lane (pend0, pend1) and runs, per wave
+// iteration, either a box phase (lanes with nothing pending) or a sphere phase (lanes with a pending
+// sphere: one test each), whichever has more lanes.  A lane's own order is untouched: its pending
+// spheres are tested before its next box test, in the reference's order, against the same t_max.
+RT_D void dfs_advance(const Book1View &V, const uint16_t *stack, Lane &L) {  // pop, next root, or exhausted
+  const int top = L.sp - 1;
+  const uint32_t popped = stack[(top > 0 ? top : 0) * kBlock];
+  if (top >= 0) {
+    L.sp = top;
+    L.cur = popped;
+  } else if (++L.k < V.n_root) {
+    L.cur = V.root_items[L.k];
+  } else {
+    L.cur = 0xffffu;
+  }
+}
+
+// Box phase of one lane (nothing pending, cur is a node or a root-list sphere).
+RT_D void box_step_v6(const Book1View &V, const float4 *nodes3, uint16_t *stack, Lane &L, float tmin) {
+  const uint32_t cur = L.cur;
+  if (__builtin_expect((cur & kLeafBit) != 0, 0)) {  // a sphere directly in the root list
+    L.pend0 = cur;
+    dfs_advance(V, stack, L);
+    return;
+  }
+  const float4 a = nodes3[2 * cur], b = nodes3[2 * cur + 1];
+  const bool hit = aabb_packed(a, b, L, tmin);
+  const uint32_t l = __float_as_uint(b.z), r = __float_as_uint(b.w);
+  const bool lleaf = (l & kLeafBit) != 0, rleaf = (r & kLeafBit) != 0;  // kNone has the leaf bit
+  L.pend0 = hit && lleaf ? l : 0xffffu;
+  L.pend1 = hit && lleaf && rleaf ? r : 0xffffu;
+  const bool moved = hit && !(lleaf && rleaf);
+  stack[L.sp * kBlock] = (uint16_t)r;  // free slot: kept only on a real push
+  L.sp += (hit && !lleaf && r != 0xffffu) ? 1 : 0;
+  if (moved)
+    L.cur = lleaf ? r : l;
+  else
+    dfs_advance(V, stack, L);
+}
+
+// Sphere phase of one lane (pend0 set): test it, shift the queue.
+RT_D void sphere_step_v6(const float4 *sph, Lane &L, float tmin) {
+  sphere_test_v5(sph, L.pend0, L, tmin);
+  L.pend0 = L.pend1;
+  L.pend1 = 0xffffu;
+}
+
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
+constexpr int kNumStats = 22;
 constexpr int kSteps = 4;
 
 // kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
 // accumulated into V.stats with one atomic per lane at exit; never used for timing.
-template <bool kLds, bool kStats = false>
+template <bool kLds, bool kStats = false, int kStep = 5>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
   const int W = V.S.cam.width;
@@ -492,8 +663,20 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   int mode = kWait;
   bool have_result = false;  // false: this lane first needs a pixel
   // stats: 0 trav iterations seen, 1 useful trav steps, 2 shade iterations seen, 3 shading lanes,
-  //        4 rays traced, 5 node visits, 6 leaf tests, 7 shade passes where this lane was idle
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  //        4 rays traced, 5 node visits, 6 root-leaf steps, 7 shade passes where this lane was idle,
+  //        8/9 shader clocks in traversal / shading iterations (wave-level, counted by lane 0 of
+  //        the wave), 10/11 wave-level traversal / shading iterations, 12/13 (v6) wave-level box /
+  //        sphere phases, (v5) sphere tests on the fast / exact-fallback path, 14 (v5) wave-level
+  //        executions of the sphere code, 15 (v5) wave-level executions of the fallback,
+  //        16/17 clock64 / wall_clock64 ticks over the wave's lifetime (lane 0), 18/19 earliest
+  //        wave start / latest wave end, 20 latest wave start, 21 first time the pixel counter ran
+  //        dry (wall_clock64; the host presets 18 and 21 to ~0)
+  unsigned long long st[kNumStats] = {};
+  long long t_iter = kStats ? (long long)clock64() : 0;
+  const long long t_start = t_iter, w_start = kStats ? (long long)wall_clock64() : 0;
+  int last_kind = -1;  // kind of the previous wave iteration (0 traversal, 1 shading)
+  uint32_t px_steps = 0;
+  long long px_t0 = 0;
   int64_t pix = 0;
   int i = 0, j = 0, s = 0, depth = 0;
   Pcg32 g;
@@ -504,28 +687,63 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   R.r0 = R.r1 = 0;
   R.n = 0;
   Lane L;
-  L.o = L.d = L.inv = mk(0, 0, 0);
-  L.a = L.tmax = 0.0f;
+  L.ox = L.oy = L.oz = L.dx = L.dy = L.dz = L.ix = L.iy = L.iz = 0.0f;
+  L.a = L.tmax = L.ra = 0.0f;
+  L.fast = false;
   L.hit = -1;
   L.cur = 0;
+  L.pend0 = L.pend1 = 0xffffu;
   L.sp = L.k = 0;
 
   for (;;) {
     const uint64_t trav = __ballot(mode == kTrav);
     const uint64_t wait = __ballot(mode == kWait);
+    if (kStats) {  // wave-uniform point: charge the clocks since the last one to the previous iteration
+      const long long now = (long long)clock64();
+      if (lane == 0 && last_kind >= 0) st[8 + last_kind] += now - t_iter, st[10 + last_kind]++;
+      t_iter = now;
+    }
     if ((trav | wait) == 0) break;
-    if (trav != 0 && (int)__popcll(wait) < V.shade_batch) {
+    // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
+    // 3/4 of them do, so a long path is not held back behind its wave's last traversals
+    const int live = (int)__popcll(trav | wait);
+    const int batch = min(V.shade_batch, (3 * live + 3) / 4);
+    const bool do_trav = trav != 0 && (int)__popcll(wait) < batch;
+    if (kStats) last_kind = do_trav ? 0 : 1;
+    if (do_trav) {
       // ---------------- traversal steps for every lane still traversing
       if (kStats && mode != kExit) st[0] += kSteps;
-      if (mode == kTrav) {
+      if (kStep == 6) {
+#pragma unroll
+        for (int u = 0; u < kSteps; u++) {
+          const bool pending = L.pend0 != 0xffffu;
+          const uint64_t sph_lanes = __ballot(mode == kTrav && pending);
+          const uint64_t box_lanes = __ballot(mode == kTrav && !pending);
+          const bool sphere_phase = box_lanes == 0 || (int)__popcll(sph_lanes) >= V.sphere_batch;
+          if (kStats && lane == 0) st[sphere_phase ? 13 : 12]++;
+          if (sphere_phase) {
+            if (mode == kTrav && pending) {
+              if (kStats) st[1]++, st[6]++, px_steps++;
+              sphere_step_v6(sph, L, tmin);
+            }
+          } else if (mode == kTrav && !pending) {
+            if (kStats) st[1]++, st[5]++, px_steps++;
+            box_step_v6(V, nodes3, stack, L, tmin);
+          }
+          if (mode == kTrav && L.pend0 == 0xffffu && L.cur == 0xffffu) mode = kWait;
+        }
+      } else if (mode == kTrav) {
 #pragma unroll
         for (int u = 0; u < kSteps; u++)
           if (mode == kTrav) {
             if (kStats) {
               st[1]++;
+              px_steps++;
               if (L.cur & kLeafBit) st[6]++; else st[5]++;
             }
-            if (trav_step(V, nodes3, sph, stack, L, tmin)) mode = kWait;
+            const bool done = kStep == 5 ? trav_step_v5<kStats>(V, nodes3, sph, stack, L, tmin, st)
+                                         : trav_step(V, nodes3, sph, stack, L, tmin);
+            if (done) mode = kWait;
           }
       }
       continue;
@@ -545,15 +763,16 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         path_done = true;
       } else {
         const rt_sphere &sp = V.S.spheres[L.hit];
-        const f3 p = ray_at(L.o, L.d, L.tmax);
+        const f3 d = mk(L.dx, L.dy, L.dz);
+        const f3 p = ray_at(mk(L.ox, L.oy, L.oz), d, L.tmax);
         const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
-        const bool front = dot(L.d, outward) < 0.0f;
+        const bool front = dot(d, outward) < 0.0f;
         const f3 normal = front ? outward : neg(outward);
         const FastMat &m = V.mats[sp.material];
-        const f3 nd = scatter(m, normal, front, L.d, g);
+        const f3 nd = scatter(m, normal, front, d, g);
         rec_push(V, R, (uint32_t)sp.material, glane);
-        L.o = p;
-        L.d = nd;
+        L.ox = p.x, L.oy = p.y, L.oz = p.z;
+        L.dx = nd.x, L.dy = nd.y, L.dz = nd.z;
         depth--;
         path_done = depth <= 0;  // the next call would return 0 at depth 0 (src/raytracing.c:40)
       }
@@ -562,6 +781,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         s++;
         if (s == spp) {  // quantize (src/raytracing.c:127-131)
           write_pixel(out + pix * 3, acc, spp);
+          if (kStats) {
+            V.pixel_cost[2 * pix] = px_steps;
+            V.pixel_cost[2 * pix + 1] = (uint32_t)((long long)wall_clock64() - px_t0);
+          }
           need_pixel = true;
         } else {
           need_sample = true;
@@ -577,9 +800,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         base = __shfl(base, first);
         pix = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
         if (pix >= total) {
+          if (kStats && mode != kExit) atomicMin(&V.stats[21], (unsigned long long)wall_clock64());
           mode = kExit;
           break;
         }
+        if (V.reverse) pix = total - 1 - pix;  // bottom rows (ground, spheres: long paths) first
         const int jj = (int)(pix / W);
         i = (int)(pix - (int64_t)jj * W);
         j = V.row0 + jj * V.row_stride;
@@ -587,6 +812,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         acc = mk(0.0f, 0.0f, 0.0f);
         s = 0;
         need_pixel = false;
+        if (kStats) px_steps = 0, px_t0 = (long long)wall_clock64();
       }
       // camera ray (src/raytracing.c:96-122)
       const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
@@ -602,8 +828,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         o = add(add(lf, scale(ld3(cam.disc_u), a)), scale(ld3(cam.disc_v), b));
       }
-      L.o = o;
-      L.d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+      const f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+      L.ox = o.x, L.oy = o.y, L.oz = o.z;
+      L.dx = d.x, L.dy = d.y, L.dz = d.z;
       depth = max_depth;
       R.n = 0;
       need_sample = false;
@@ -620,19 +847,32 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     }
     if (mode == kExit) continue;
     // set up the traversal of the new ray
-    L.inv = mk(1.0f / L.d.x, 1.0f / L.d.y, 1.0f / L.d.z);
-    L.a = dot(L.d, L.d);
+    L.ix = 1.0f / L.dx, L.iy = 1.0f / L.dy, L.iz = 1.0f / L.dz;
+    L.a = dot(mk(L.dx, L.dy, L.dz), mk(L.dx, L.dy, L.dz));
+    L.fast = L.a >= kDivLo && L.a <= kDivHi;
+    L.ra = recip_core(L.a);
     L.tmax = __builtin_inff();
     L.hit = -1;
     L.sp = 0;
     L.k = 0;
     L.cur = V.root_items[0];
+    L.pend0 = L.pend1 = 0xffffu;
     have_result = true;
     if (kStats) st[4]++;
     mode = V.n_root > 0 ? kTrav : kWait;
   }
-  if (kStats)
-    for (int q = 0; q < 8; q++) atomicAdd(&V.stats[q], st[q]);
+  if (kStats) {
+    if (lane == 0) {  // 16/17: clock64 and wall_clock64 (100 MHz) ticks over the wave's lifetime
+      st[16] = (long long)clock64() - t_start;
+      st[17] = (long long)wall_clock64() - w_start;
+    }
+    for (int q = 0; q < 18; q++) atomicAdd(&V.stats[q], st[q]);
+    if (lane == 0) {  // 18/19: earliest wave start, latest wave end (wall_clock64 ticks)
+      atomicMin(&V.stats[18], (unsigned long long)w_start);
+      atomicMax(&V.stats[19], (unsigned long long)wall_clock64());
+      atomicMax(&V.stats[20], (unsigned long long)w_start);
+    }
+  }
 }
 
 }  // namespace b1

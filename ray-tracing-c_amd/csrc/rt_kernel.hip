@@ -60,13 +60,12 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
 }
 
 // Persistent Book-1 kernel (rt_book1.h): grid = resident workgroups, lanes steal pixels.
-template <bool kLds, int kVer>
-__global__ __launch_bounds__(b1::kBlock) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+// kOcc > 0: ask the register allocator for that many waves per SIMD (launch-bounds minimum).
+template <bool kLds, int kVer, bool kStats = false, int kOcc = 0>
+__global__ __launch_bounds__(b1::kBlock, kOcc > 0 ? kOcc : 1) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (kVer == 4)  // diagnostic: v3 with per-lane counters
-    b1::render_batched<kLds, true>(V, out, lds);
-  else if (kVer == 3)
-    b1::render_batched<kLds>(V, out, lds);
+  if (kVer >= 3)  // batched megaloop; kStep 3 / 5 / 6 = traversal step generation
+    b1::render_batched<kLds, kStats, kVer>(V, out, lds);
   else
     b1::render<kLds>(V, out, lds);
 }
@@ -93,6 +92,70 @@ __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t 
   }
 }
 
+// Exactness checks of the Book-1 v5 arithmetic (rt_book1.h: sqrt_core / div_core / sphere_test_v5)
+// against what the compiler emits for sqrtf() and '/' -- run on the device, count mismatches.
+//  fn 0: sqrt_core(x) vs sqrtf(x), x = the float with bits start + k, where x is in the core's domain
+//  fn 1: div_core vs '/' on hashed pairs (a in [kDivLo, kDivHi], |x| in [2^-40, kNumHi] or 0)
+//  fn 2: sphere_test_v5 vs the v3 sphere test (outcome: hit index and t_max bits) on hashed rays,
+//        half of them starting on the sphere's surface (the scattered-ray case: c ~ 0)
+RT_D uint64_t diag_hash(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+RT_D float diag_float(uint64_t h, int emin, int emax) {  // random sign/mantissa, exponent in [emin, emax]
+  const int e = emin + (int)((h >> 40) % (uint64_t)(emax - emin + 1));
+  return __uint_as_float((uint32_t)((h >> 63) << 31) | (uint32_t)((e + 127) << 23) | (uint32_t)(h & 0x7fffff));
+}
+__global__ void rt_diag_arith_kernel(int fn, uint64_t start, uint64_t count, uint64_t seed,
+                                     unsigned long long *mism) {
+  unsigned long long bad = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (uint64_t)gridDim.x * blockDim.x) {
+    if (fn == 0) {
+      const float x = __uint_as_float((uint32_t)(start + k));
+      if (!(x == 0.0f || (x >= b1::kSqrtLo && x <= __FLT_MAX__))) continue;
+      bad += __float_as_uint(b1::sqrt_core(x)) != __float_as_uint(sqrtf(x));
+    } else if (fn == 1) {
+      const uint64_t h1 = diag_hash(seed ^ (start + k)), h2 = diag_hash(h1);
+      const float a = fabsf(diag_float(h1, -20, 19));
+      float x = diag_float(h2, -40, 39);
+      if ((h2 & 0xff00000) == 0) x = 0.0f;
+      bad += __float_as_uint(b1::div_core(x, a, b1::recip_core(a))) != __float_as_uint(x / a);
+    } else {
+      const uint64_t h1 = diag_hash(seed ^ (start + k)), h2 = diag_hash(h1), h3 = diag_hash(h2), h4 = diag_hash(h3);
+      const float4 sph = make_float4(diag_float(h1, -2, 3), diag_float(h1 >> 7, -2, 3), diag_float(h1 >> 13, -2, 3), 0.0f);
+      const float r = fabsf(diag_float(h2, -4, 9));
+      float4 sp = sph;
+      sp.w = r * r;
+      f3 d = mk(diag_float(h3, -3, 2), diag_float(h3 >> 9, -3, 2), diag_float(h3 >> 17, -3, 2));
+      f3 o;
+      if (h4 & 1) {  // on the surface (up to rounding), like a scattered ray
+        const float inv = 1.0f / sqrtf(dot(d, d));
+        const f3 n = mk(d.z * inv, d.x * inv, d.y * inv);
+        o = add(mk(sph.x, sph.y, sph.z), scale(n, r));
+      } else {
+        o = mk(diag_float(h4, -3, 6), diag_float(h4 >> 11, -3, 6), diag_float(h4 >> 21, -3, 6));
+      }
+      b1::Lane A;
+      A.ox = o.x, A.oy = o.y, A.oz = o.z, A.dx = d.x, A.dy = d.y, A.dz = d.z;
+      A.ix = A.iy = A.iz = 0.0f;
+      A.a = dot(d, d);
+      A.ra = b1::recip_core(A.a);
+      A.fast = A.a >= b1::kDivLo && A.a <= b1::kDivHi;
+      A.tmax = (h4 & 2) ? __builtin_inff() : fabsf(diag_float(h4 >> 5, -4, 10));
+      A.hit = -1;
+      A.cur = 0;
+      A.sp = A.k = 0;
+      b1::Lane B = A;
+      b1::sphere_test_v5(&sp, 0, A, 1e-3f);
+      b1::sphere_test_lane(&sp, 0, B, 1e-3f);
+      bad += (A.hit != B.hit) || (__float_as_uint(A.tmax) != __float_as_uint(B.tmax));
+    }
+  }
+  if (bad) atomicAdd(mism, bad);
+}
+
 // ------------------------------------------------------------------------------ device scene
 struct rt_device_scene {
   int device;
@@ -104,7 +167,9 @@ struct rt_device_scene {
   // Book-1 fast path (rt_book1.h), when the scene qualifies
   bool book1 = false;
   bool book1_lds = false;
-  int book1_ver = 3;
+  int book1_ver = 5;
+  int book1_occ = 0;         // register-allocation occupancy target of the launched variant (0: default)
+  bool book1_stats = false;  // diagnostic counters build (RT_BOOK1_STATS=1)
   b1::Book1View b1view;
   void *b1_arena = nullptr;
   int b1_grid = 0;
@@ -296,31 +361,43 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const size_t scene_bytes = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
   {
     const char *ev = getenv("RT_BOOK1_V");
-    d->book1_ver = (ev && *ev == '2') ? 2 : 3;
-    if (env_flag("RT_BOOK1_STATS", false)) d->book1_ver = 4;
+    d->book1_ver = (ev && *ev) ? atoi(ev) : 5;
+    if (d->book1_ver != 2 && d->book1_ver != 3 && d->book1_ver != 6) d->book1_ver = 5;
   }
-  // v2 keeps 32-bit stack slots, v3 16-bit ones
-  const size_t stack_bytes = (size_t)b1::kStackSlots * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
+  // v2 keeps 32-bit stack slots, v3+ 16-bit ones (+1 slot: v5+ store the right child unconditionally)
+  // only the slots this scene's DFS can reach (host-computed `need` <= kStackSlots) take LDS
+  const size_t stack_bytes = (size_t)(need + 1) * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
   d->book1_lds = env_flag("RT_BOOK1_LDS", true) && scene_bytes + stack_bytes <= 64 * 1024;
+  d->book1_stats = env_flag("RT_BOOK1_STATS", false) && d->book1_ver >= 5 && d->book1_lds;
   d->b1_lds_bytes = align_up((d->book1_lds ? scene_bytes : 0) + stack_bytes, 16);
 
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0;
-  const void *fn = d->book1_ver == 4   ? (const void *)rt_book1_kernel<true, 4>
+  {
+    const char *eo = getenv("RT_BOOK1_OCC");
+    d->book1_occ = (eo && *eo) ? atoi(eo) : 0;
+    if (d->book1_ver != 5 || d->book1_stats || (d->book1_occ != 5 && d->book1_occ != 6)) d->book1_occ = 0;
+  }
+  const void *fn = d->book1_stats ? (d->book1_ver == 6 ? (const void *)rt_book1_kernel<true, 6, true>
+                                                       : (const void *)rt_book1_kernel<true, 5, true>)
+                   : d->book1_occ == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 5> : (const void *)rt_book1_kernel<false, 5, false, 5>)
+                   : d->book1_occ == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 6> : (const void *)rt_book1_kernel<false, 5, false, 6>)
+                   : d->book1_ver == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 6> : (const void *)rt_book1_kernel<false, 6>)
+                   : d->book1_ver == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>)
                    : d->book1_ver == 3 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 3> : (const void *)rt_book1_kernel<false, 3>)
                                        : (d->book1_lds ? (const void *)rt_book1_kernel<true, 2> : (const void *)rt_book1_kernel<false, 2>);
-  if (d->book1_ver == 4) d->book1_lds = true;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, b1::kBlock, d->b1_lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->b1_grid = prop.multiProcessorCount * per_cu;
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth - b1::kRecRegs) * spill_lanes * sizeof(uint16_t);
 
-  size_t off[6], total = 0;
-  const size_t sizes[6] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
-                           roots.size() * sizeof(uint16_t), 256, spill_bytes};  // [4]: counter + 8 stats
-  for (int k = 0; k < 6; k++) {
+  size_t off[7], total = 0;
+  const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
+  const size_t sizes[7] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+                           roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes};  // [4]: counter + stats
+  for (int k = 0; k < 7; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -341,6 +418,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.work_counter = (int32_t *)(b + off[4]);
   V.stats = (unsigned long long *)(b + off[4] + 64);
   V.spill = (uint16_t *)(b + off[5]);
+  V.pixel_cost = d->book1_stats ? (uint32_t *)(b + off[6]) : nullptr;
   V.spill_lanes = spill_lanes;
   V.n_nodes = s->n_bvh;
   V.n_spheres = s->n_spheres;
@@ -348,8 +426,13 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.stack_need = need;
   {
     const char *eb = getenv("RT_SHADE_BATCH");
-    V.shade_batch = (eb && *eb) ? atoi(eb) : 32;
+    V.shade_batch = (eb && *eb) ? atoi(eb) : 48;
     V.shade_batch = V.shade_batch < 1 ? 1 : (V.shade_batch > 64 ? 64 : V.shade_batch);  // >= 1: progress
+    const char *eo = getenv("RT_PIXEL_ORDER");
+    V.reverse = (eo && !strcmp(eo, "rev")) ? 1 : 0;
+    const char *es = getenv("RT_SPHERE_BATCH");
+    V.sphere_batch = (es && *es) ? atoi(es) : 16;
+    V.sphere_batch = V.sphere_batch < 1 ? 1 : (V.sphere_batch > 64 ? 64 : V.sphere_batch);
   }
   d->book1 = true;
   return 0;
@@ -445,21 +528,32 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     V.row0 = row0;
     V.row_stride = row_stride;
     V.n_rows = n_rows;
-    HIP_OK(hipMemsetAsync(V.work_counter, 0, d->book1_ver == 4 ? 256 : sizeof(int32_t), st));
-    const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-    if (d->book1_ver == 4) {
-      hipLaunchKernelGGL((rt_book1_kernel<true, 4>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-    } else if (d->book1_ver == 3) {
-      if (d->book1_lds)
-        hipLaunchKernelGGL((rt_book1_kernel<true, 3>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-      else
-        hipLaunchKernelGGL((rt_book1_kernel<false, 3>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-    } else {
-      if (d->book1_lds)
-        hipLaunchKernelGGL((rt_book1_kernel<true, 2>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-      else
-        hipLaunchKernelGGL((rt_book1_kernel<false, 2>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    HIP_OK(hipMemsetAsync(V.work_counter, 0, d->book1_stats ? 256 : sizeof(int32_t), st));
+    if (d->book1_stats) {
+      HIP_OK(hipMemsetAsync(V.stats + 18, 0xff, sizeof(unsigned long long), st));
+      HIP_OK(hipMemsetAsync(V.stats + 21, 0xff, sizeof(unsigned long long), st));
     }
+    const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
+#define RT_B1_LAUNCH(LDS, VER, ST, ...) \
+  hipLaunchKernelGGL((rt_book1_kernel<LDS, VER, ST, ##__VA_ARGS__>), g1, blk, d->b1_lds_bytes, st, V, d_out)
+    switch (d->book1_occ * 100 + d->book1_ver * 4 + (d->book1_lds ? 1 : 0) + (d->book1_stats ? 2 : 0)) {
+      case 500 + 5 * 4 + 1: RT_B1_LAUNCH(true, 5, false, 5); break;
+      case 500 + 5 * 4 + 0: RT_B1_LAUNCH(false, 5, false, 5); break;
+      case 600 + 5 * 4 + 1: RT_B1_LAUNCH(true, 5, false, 6); break;
+      case 600 + 5 * 4 + 0: RT_B1_LAUNCH(false, 5, false, 6); break;
+      case 6 * 4 + 3: RT_B1_LAUNCH(true, 6, true); break;
+      case 5 * 4 + 3: RT_B1_LAUNCH(true, 5, true); break;
+      case 6 * 4 + 1: RT_B1_LAUNCH(true, 6, false); break;
+      case 6 * 4 + 0: RT_B1_LAUNCH(false, 6, false); break;
+      case 5 * 4 + 1: RT_B1_LAUNCH(true, 5, false); break;
+      case 5 * 4 + 0: RT_B1_LAUNCH(false, 5, false); break;
+      case 3 * 4 + 1: RT_B1_LAUNCH(true, 3, false); break;
+      case 3 * 4 + 0: RT_B1_LAUNCH(false, 3, false); break;
+      case 2 * 4 + 1: RT_B1_LAUNCH(true, 2, false); break;
+      case 2 * 4 + 0: RT_B1_LAUNCH(false, 2, false); break;
+      default: return rt_set_error("book1 variant %d not built", d->book1_ver), -1;
+    }
+#undef RT_B1_LAUNCH
     HIP_OK(hipGetLastError());
     return 0;
   }
@@ -550,11 +644,12 @@ extern "C" int rt_render(const rt_flat_scene *s, int n_gpus, uint8_t *out_host) 
   return rc;
 }
 
-// Diagnostic counters of the last RT_BOOK1_STATS=1 launch on this scene (8 x u64; see rt_book1.h).
-extern "C" int rt_book1_stats(rt_device_scene *d, unsigned long long *out8) {
-  if (!d || !d->book1 || d->book1_ver != 4) return rt_set_error("no stats build active (RT_BOOK1_STATS=1)"), -1;
+// Diagnostic counters of the last RT_BOOK1_STATS=1 launch on this scene (b1::kNumStats x u64; see rt_book1.h).
+extern "C" int rt_book1_stats(rt_device_scene *d, unsigned long long *out, int n) {
+  if (!d || !d->book1 || !d->book1_stats) return rt_set_error("no stats build active (RT_BOOK1_STATS=1)"), -1;
   HIP_OK(hipSetDevice(d->device));
-  HIP_OK(hipMemcpy(out8, d->b1view.stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (n < 0 || n > b1::kNumStats) return rt_set_error("rt_book1_stats: n must be in [0, %d]", b1::kNumStats), -1;
+  HIP_OK(hipMemcpy(out, d->b1view.stats, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -571,5 +666,28 @@ extern "C" int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_
   HIP_OK(hipMemcpy(out_host, dy, nout * sizeof(float), hipMemcpyDeviceToHost));
   HIP_OK(hipFree(dx));
   HIP_OK(hipFree(dy));
+  return 0;
+}
+
+extern "C" int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches,
+                             int device) {
+  if (fn < 0 || fn > 2 || mismatches == NULL) return rt_set_error("rt_diag_arith: bad arguments"), -1;
+  HIP_OK(hipSetDevice(device));
+  unsigned long long *dm = NULL;
+  HIP_OK(hipMalloc(&dm, sizeof *dm));
+  HIP_OK(hipMemset(dm, 0, sizeof *dm));
+  hipLaunchKernelGGL(rt_diag_arith_kernel, dim3(4096), dim3(256), 0, 0, fn, start, count, seed, dm);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpy(mismatches, dm, sizeof *dm, hipMemcpyDeviceToHost));
+  HIP_OK(hipFree(dm));
+  return 0;
+}
+
+extern "C" int rt_book1_pixel_cost(rt_device_scene *d, uint32_t *out, int64_t n_items) {
+  if (!d || !d->book1 || !d->book1_stats) return rt_set_error("no stats build active (RT_BOOK1_STATS=1)"), -1;
+  if (n_items < 0 || n_items > (int64_t)d->width * d->height) return rt_set_error("rt_book1_pixel_cost: bad count"), -1;
+  HIP_OK(hipSetDevice(d->device));
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(out, d->b1view.pixel_cost, (size_t)n_items * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return 0;
 }

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_void_p
 
 import numpy as np
@@ -73,12 +74,29 @@ assert RtFlatScene.n_image_bytes.offset == 192
 _lib = None
 
 
+def _init_torch_runtime_first() -> None:
+    """The PyTorch-ROCm wheel bundles its own HIP runtime (torch/lib/libamdhip64.so, no SONAME), so a
+    process holding PyTorch and this library runs two HIP runtimes side by side.  PyTorch's only
+    finds the GPUs when it initialises first (measured on MI355X: the other order gives "No HIP GPUs
+    are available"), so when PyTorch is already imported it is initialised before this library's
+    first HIP call.  Processes that import PyTorch later must initialise it before using rtc."""
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # a CPU-only torch build: nothing to order
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load librtc_amd.so (built by ``make -C ray-tracing-c_amd``)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RtcError(f"{LIB_PATH} not built: run `make -C ray-tracing-c_amd` (or __graft_entry__.build())")
+        _init_torch_runtime_first()
         L = ctypes.CDLL(LIB_PATH)
         P = POINTER(RtFlatScene)
         L.rt_scene_preset.argtypes = [c_int, c_int, c_int, c_int]
@@ -98,6 +116,8 @@ def lib() -> ctypes.CDLL:
         L.rt_last_kernel_ms.restype = c_double
         L.rt_diag_libm.argtypes = [c_int, c_void_p, c_void_p, c_int64, c_int]
         L.rt_diag_libm.restype = c_int
+        L.rt_diag_arith.argtypes = [c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_int]
+        L.rt_diag_arith.restype = c_int
         L.rt_last_error.restype = c_char_p
         L.rt_abi_version.restype = c_int
         _lib = L
@@ -224,6 +244,17 @@ def assemble_frame(parts, height: int, world: int) -> np.ndarray:
         row0, stride, n = rows_of(height, r, world)
         frame[row0::stride][:n] = np.asarray(p)[:n]
     return frame
+
+
+def diag_arith(fn: int, start: int, count: int, seed: int = 0, device: int = 0) -> int:
+    """Mismatch count of the Book-1 kernel's exact arithmetic cores vs the compiler's sqrtf / '/':
+    0 sqrt over float bit patterns [start, start+count), 1 division on hashed pairs, 2 sphere-hit
+    outcome on hashed rays (rt_hip.h: rt_diag_arith)."""
+    out = ctypes.c_ulonglong(0)
+    rc = lib().rt_diag_arith(int(fn), int(start), int(count), int(seed), ctypes.byref(out), int(device))
+    if rc != 0:
+        raise RtcError(f"rt_diag_arith failed: {last_error()}")
+    return int(out.value)
 
 
 def diag_libm(fn: int, x: np.ndarray, device: int = 0) -> np.ndarray:

@@ -9,6 +9,7 @@ import subprocess
 import sys
 
 import pytest
+import torch  # noqa: F401  (imported before rtc loads its HIP runtime: see rtc._init_torch_runtime_first)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ray-tracing-c_amd")

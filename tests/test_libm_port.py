@@ -111,3 +111,22 @@ def test_device_atan2f_acosf_sphere_uv():
                         np.array([-1.0, 1.0, 0.0, -0.0, 0.5, -0.5], np.float32)])
     ok = _same_bits(rtc.diag_libm(5, a), _host("ref_acosf", a, a.size))
     assert ok.all(), f"acosf: {(~ok).sum()} mismatches"
+
+
+@pytest.mark.gpu
+def test_device_exact_sqrt_core_all_floats():
+    """Book-1 v5 sqrt_core == sqrtf on every float of its domain (0 and [2^-96, inf])."""
+    assert rtc.diag_arith(0, 0, 0x7F800001) == 0
+
+
+@pytest.mark.gpu
+def test_device_exact_div_core_random_pairs():
+    """Book-1 v5 div_core with the per-ray reciprocal == '/' on 2^32 hashed pairs of its domain."""
+    assert rtc.diag_arith(1, 0, 1 << 32, seed=11) == 0
+
+
+@pytest.mark.gpu
+def test_device_sphere_test_v5_matches_reference_expression():
+    """The guarded fast sphere test gives the reference's outcome (hit, t_max bits) on 2^30 hashed rays,
+    half starting on the sphere (c ~ 0: cancelling numerators, the tiny-root argument in rt_book1.h)."""
+    assert rtc.diag_arith(2, 0, 1 << 30, seed=5) == 0
