@@ -28,6 +28,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kStackSlots = 16;   // per-lane DFS slots in LDS, 32-bit (host checks the need)
 constexpr int kRecRegs = 8;       // path-record slots held in registers (4 x 16-bit per u64)
 constexpr uint16_t kLeafBit = 0x8000;  // 16-bit ref: leaf sphere index | kLeafBit, else node index
+constexpr uint16_t kHasLeaf7 = 0x4000; // v7 node refs: the node has a leaf child (its record's spheres are read)
 
 struct FastMat {   // 32 B: material resolved to what the Book-1 path needs
   float albedo[3];  // Solid texture colour; (1,1,1) for Dielectric
@@ -49,9 +50,14 @@ struct Book1View {
   int32_t shade_batch;       // v3+: shade once this many lanes of a wave are waiting
   int32_t sphere_batch;      // v6: run a sphere phase once this many lanes have a pending sphere
   int32_t reverse;           // hand out work items last-first
+  int32_t coop_lanes;        // v5: cooperative traversal once the counter is dry and <= this many lanes live
+  int32_t experiment;        // stats builds only: timing experiments that change the image (RT_EXPERIMENT)
   unsigned long long *stats; // diagnostic counters (kStats builds only)
   uint32_t *pixel_cost;      // kStats: per work item {traversal steps, wall_clock64 ticks}
   uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
+  const float4 *nodes7_g;    // v7: 4 float4 per record (Node7 below), then one all-zero dummy record
+  const uint16_t *root7_items;
+  int32_t n_nodes7;          // records incl. the dummy
   int32_t spill_lanes;
 };
 
@@ -502,6 +508,7 @@ RT_D bool trav_step_v5(const Book1View &V, const float4 *nodes3, const float4 *s
   } else {
     const float4 a = nodes3[2 * cur], b = nodes3[2 * cur + 1];
     const bool hit = aabb_packed(a, b, L, tmin);
+    if (kStats && hit) st[22]++;
     const uint32_t l = __float_as_uint(b.z), r = __float_as_uint(b.w);
     const bool lleaf = (l & kLeafBit) != 0, rleaf = (r & kLeafBit) != 0;  // kNone has the leaf bit
     t0 = hit && lleaf ? l : 0xffffu;
@@ -511,6 +518,7 @@ RT_D bool trav_step_v5(const Book1View &V, const float4 *nodes3, const float4 *s
     L.sp += (hit && !lleaf && r != 0xffffu) ? 1 : 0;
     L.cur = moved ? (lleaf ? r : l) : cur;
   }
+  if (kStats && (V.experiment & 1)) t0 = t1 = 0xffffu;  // timing experiment: no sphere tests
   if (t0 != 0xffffu) {
     if (kStats && __lane_id() == __builtin_ctzll(__ballot(1))) st[14]++;
     sphere_test_v5<kStats>(sph, t0, L, tmin, st);
@@ -578,6 +586,109 @@ RT_D bool trav_step(const Book1View &V, const float4 *nodes3, const float4 *sph,
   return true;
 }
 
+// ---------------------------------------------------------------- v7: one LDS round trip per step
+// Per-step latency, not lane occupancy, bounds the v5 loop: a lone wave spends ~1250 clocks per DFS
+// step (issue of ~100 VALU + ~40 SALU at 4 clocks each, 4-5 dependent LDS round trips, ~11 exec-mask
+// branches).  v7 lays each node out with everything the step can need (Node7, 64 B):
+//   q0 = (lo.x, hi.x, lo.y, hi.y)   q1 = (lo.z, hi.z, left ref, right ref)
+//   q2 = (cx_l, cx_r, cy_l, cy_r)   q3 = (cz_l, cz_r, r2_l, r2_r)     (leaf children's spheres)
+// so a step issues all its LDS reads at once (node + speculative stack pop), tests both leaf spheres
+// with packed f32 math, and picks the next node with selects.  Node refs carry kHasLeaf7 so the
+// sphere half is only fetched for nodes that have a leaf child (others read the dummy record).
+// The two spheres are evaluated independently of t_max (root r = q1 unless q1 <= t_min, then q2)
+// and then applied in the reference's order (left, then right against the updated t_max):
+// Sphere_hit's accept test `!(root <= t_min || root >= t_max)` on that r is exactly the reference's
+// two-root sequence, because q1 <= q2 (monotone rounding) makes a q1 >= t_max rejection final.
+typedef float f2v7 __attribute__((ext_vector_type(2)));
+
+// sqrt_core/div_core on a pair; `ok` false for lanes whose operands leave the cores' ranges
+RT_D void sphere_pair_roots(f2v7 b, f2v7 disc, const Lane &L, float tmin, bool &ok, f2v7 &root) {
+  const float sq0 = sqrt_core(disc.x), sq1 = sqrt_core(disc.y);
+  const f2v7 sq = {sq0, sq1};
+  const f2v7 n1 = -b - sq, n2 = -b + sq;
+  float la = L.a, lra = L.ra;
+  asm volatile("" : "+v"(la), "+v"(lra));
+  const f2v7 a = {la, la}, ra = {lra, lra};
+  f2v7 q0 = n1 * ra;
+  f2v7 q1 = __builtin_elementwise_fma(__builtin_elementwise_fma(-a, q0, n1), ra, q0);
+  const f2v7 r1 = __builtin_elementwise_fma(__builtin_elementwise_fma(-a, q1, n1), ra, q1);
+  q0 = n2 * ra;
+  q1 = __builtin_elementwise_fma(__builtin_elementwise_fma(-a, q0, n2), ra, q0);
+  const f2v7 r2 = __builtin_elementwise_fma(__builtin_elementwise_fma(-a, q1, n2), ra, q1);
+  ok = (int)L.fast & (int)((disc.x == 0.0f) | ((disc.x >= kSqrtLo) & (disc.x <= __FLT_MAX__))) &
+       (int)((disc.y == 0.0f) | ((disc.y >= kSqrtLo) & (disc.y <= __FLT_MAX__))) &
+       (int)(fmaxf(fmaxf(fabsf(n1.x), fabsf(n1.y)), fmaxf(fabsf(n2.x), fabsf(n2.y))) <= kNumHi);
+  root.x = (r1.x <= tmin) ? r2.x : r1.x;
+  root.y = (r1.y <= tmin) ? r2.y : r1.y;
+}
+
+template <bool kStats = false>
+RT_D bool trav_step_v7(const Book1View &V, const float4 *nodes7, uint16_t *stack, Lane &L, float tmin,
+                       unsigned long long *st = nullptr) {
+  const uint32_t cur = L.cur;
+  const int top = L.sp - 1;
+  const uint32_t popped = stack[(top > 0 ? top : 0) * kBlock];  // speculative pop
+  const float4 *nd = nodes7 + 4 * (cur & 0x3fffu);
+  const float4 *ns = (cur & kHasLeaf7) ? nd : nodes7 + 4 * (V.n_nodes7 - 1);  // dummy: no leaves
+  const float4 q0 = nd[0], q1 = nd[1], q2 = ns[2], q3 = ns[3];
+  const bool hit = aabb_packed(q0, q1, L, tmin);
+  const uint32_t l = __float_as_uint(q1.z), r = __float_as_uint(q1.w);
+  const bool lleaf = (l & kLeafBit) != 0, rleaf = (r & kLeafBit) != 0;  // kNone has the leaf bit
+  const bool t0 = hit && lleaf, t1 = t0 && rleaf && r != 0xffffu;
+  if (t0) {
+    if (kStats && __lane_id() == __builtin_ctzll(__ballot(1))) st[14]++;
+    // Sphere_hit (src/hittable.c:120-151) for the pair (left, right), packed
+    const f2v7 cx = {q2.x, q2.y}, cy = {q2.z, q2.w}, cz = {q3.x, q3.y}, r2 = {q3.z, q3.w};
+    // register copies of the lane's ray: splatting struct fields straight into vector ops lets the
+    // vectorizer widen them into overlapping loads of the Lane struct, which then stays in scratch
+    float ox = L.ox, oy = L.oy, oz = L.oz, dx = L.dx, dy = L.dy, dz = L.dz, a = L.a;
+    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz), "+v"(a));
+    const f2v7 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const f2v7 b = (ocx * dx + ocy * dy) + ocz * dz;
+    const f2v7 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+    const f2v7 disc = b * b - a * c;
+    bool ok;
+    f2v7 root;
+    sphere_pair_roots(b, disc, L, tmin, ok, root);
+    if (kStats) st[ok ? 12 : 13]++;
+    if (__builtin_expect(!ok, 0)) {  // the reference expressions, per sphere
+      const float s0 = sqrtf(disc.x), s1 = sqrtf(disc.y);
+      const float a0 = (-b.x - s0) / L.a, b0 = (-b.x + s0) / L.a;
+      const float a1 = (-b.y - s1) / L.a, b1v = (-b.y + s1) / L.a;
+      root.x = (a0 <= tmin) ? b0 : a0;
+      root.y = (a1 <= tmin) ? b1v : a1;
+    }
+    if (disc.x < 0.0f) root.x = -__builtin_inff();  // no root: -inf <= t_min rejects it for any t_max
+    if (disc.y < 0.0f) root.y = -__builtin_inff();
+    if (!(root.x <= tmin || root.x >= L.tmax)) {
+      L.tmax = root.x;
+      L.hit = (int32_t)(l & 0x7fffu);
+    }
+    if (t1 && !(root.y <= tmin || root.y >= L.tmax)) {
+      L.tmax = root.y;
+      L.hit = (int32_t)(r & 0x7fffu);
+    }
+  }
+  const bool moved = hit && !(lleaf && rleaf);
+  stack[L.sp * kBlock] = (uint16_t)r;  // free slot: kept only on a real push
+  const bool push = hit && !lleaf && r != 0xffffu;
+  if (moved) {
+    L.sp += push ? 1 : 0;
+    L.cur = lleaf ? r : l;
+    return false;
+  }
+  if (top >= 0) {
+    L.sp = top;
+    L.cur = popped;
+    return false;
+  }
+  if (++L.k < V.n_root) {
+    L.cur = V.root7_items[L.k];
+    return false;
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------- v6: box and sphere phases
 // v5 tests the leaf spheres of a node inside the node's step, so every wave step runs the box code
 // AND two sphere tests whenever any lane of the wave has a leaf -- with a few lanes active in the
@@ -628,8 +739,124 @@ RT_D void sphere_step_v6(const float4 *sph, Lane &L, float tmin) {
   L.pend1 = 0xffffu;
 }
 
+// ---------------------------------------------------------------- cooperative traversal (frame tail)
+// A lane renders its pixel's samples in sequence (one pcg32 stream per pixel), so the frame ends
+// with the slowest pixels' lanes running alone: measured on the headline frame, the pixel counter
+// runs dry at ~1/3 of the kernel and the rest is that tail, with per-step latency -- not lane count --
+// setting the pace.  Once the counter is dry and a wave has few live lanes, the wave traces each
+// remaining ray with all 64 lanes: every node's box interval and every sphere's root are
+// independent of t_max, so the lanes compute them all in parallel (kCoopSlots per lane), and one
+// wave-uniform walk then replays the reference's DFS (src/hittable.c:74-88, :266-277) on them:
+//   box hit at visit   <=>  !(fminf(t_max, X) <= E)   (E = fmaxf chain from t_min, X = fminf chain)
+//   sphere accepted    <=>  !(r <= t_min || r >= t_max), r = q1 unless q1 <= t_min, then q2
+// (the two-root sequence of Sphere_hit, since q1 <= q2; "no root" is -inf, rejected for any t_max).
+typedef float f8v __attribute__((ext_vector_type(8)));
+typedef unsigned int u8v __attribute__((ext_vector_type(8)));
+constexpr int kCoopSlots = 8;  // 64 x 8 = 512 nodes and 512 spheres at most
+
+RT_D float lane_bcast(float x, int src) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src)); }
+
+struct CoopRay {  // wave-uniform copy of the traced ray
+  float ox, oy, oz, dx, dy, dz, ix, iy, iz, a, ra;
+  bool fast;
+};
+
+// Sphere_hit's accepted root for this sphere, independent of t_max (see above)
+RT_D float coop_sphere_root(float4 s, const CoopRay &C, float tmin) {
+  const f3 oc = sub(mk(C.ox, C.oy, C.oz), mk(s.x, s.y, s.z));
+  const float b = dot(oc, mk(C.dx, C.dy, C.dz));
+  const float c = dot(oc, oc) - s.w;
+  const float disc = b * b - C.a * c;
+  if (disc < 0) return -__builtin_inff();
+  float sq = sqrt_core(disc);
+  float q1 = div_core(-b - sq, C.a, C.ra), q2 = div_core(-b + sq, C.a, C.ra);
+  const bool ok = (int)C.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                  (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+  if (__builtin_expect(!ok, 0)) {
+    sq = sqrtf(disc);
+    q1 = (-b - sq) / C.a;
+    q2 = (-b + sq) / C.a;
+  }
+  return (q1 <= tmin) ? q2 : q1;
+}
+
+// Trace lane `src`'s ray with the whole wave; returns (t_max, hit) of the reference's traversal.
+// `ustack` is a wave-uniform scratch stack (one column of the wave's DFS stacks, free between rays).
+RT_D void coop_trace(const Book1View &V, const float4 *nodes3, const float4 *sph, uint16_t *ustack,
+                     const Lane &L, int src, float tmin, float &out_tmax, int &out_hit) {
+  const int lane = __lane_id();
+  CoopRay C;
+  C.ox = lane_bcast(L.ox, src), C.oy = lane_bcast(L.oy, src), C.oz = lane_bcast(L.oz, src);
+  C.dx = lane_bcast(L.dx, src), C.dy = lane_bcast(L.dy, src), C.dz = lane_bcast(L.dz, src);
+  C.ix = lane_bcast(L.ix, src), C.iy = lane_bcast(L.iy, src), C.iz = lane_bcast(L.iz, src);
+  C.a = lane_bcast(L.a, src), C.ra = lane_bcast(L.ra, src);
+  C.fast = __builtin_amdgcn_readlane((int)L.fast, src) != 0;
+  // per-lane tables: node n = k*64 + lane -> (E, X, children), sphere i = k*64 + lane -> root
+  f8v E, X, R;
+  u8v CH;
+#pragma unroll
+  for (int k = 0; k < kCoopSlots; k++) {
+    const int n = k * 64 + lane;
+    float e = 0.0f, x = 0.0f, r = -__builtin_inff();
+    unsigned ch = 0xffffffffu;
+    if (n < V.n_nodes) {
+      const float4 a = nodes3[2 * n], b = nodes3[2 * n + 1];
+      const float t0x = (a.x - C.ox) * C.ix, t1x = (a.y - C.ox) * C.ix;
+      const float t0y = (a.z - C.oy) * C.iy, t1y = (a.w - C.oy) * C.iy;
+      const float t0z = (b.x - C.oz) * C.iz, t1z = (b.y - C.oz) * C.iz;
+      const float nx = C.ix < 0 ? t1x : t0x, fx = C.ix < 0 ? t0x : t1x;
+      const float ny = C.iy < 0 ? t1y : t0y, fy = C.iy < 0 ? t0y : t1y;
+      const float nz = C.iz < 0 ? t1z : t0z, fz = C.iz < 0 ? t0z : t1z;
+      e = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+      x = fminf(fminf(fx, fy), fz);
+      ch = (__float_as_uint(b.z) & 0xffffu) | (__float_as_uint(b.w) << 16);
+    }
+    if (n < V.n_spheres) r = coop_sphere_root(sph[n], C, tmin);
+    E[k] = e, X[k] = x, R[k] = r, CH[k] = ch;
+  }
+  // the reference's DFS on the tables (wave-uniform)
+  float tmax = __builtin_inff();
+  int hit = -1;
+  for (int item = 0; item < V.n_root; item++) {
+    uint32_t cur = V.root_items[item];
+    int sp = 0;
+    for (;;) {
+      if (cur & kLeafBit) {
+        const int si = (int)(cur & 0x7fffu);
+        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(R[si >> 6]), si & 63));
+        if (!(r <= tmin || r >= tmax)) tmax = r, hit = si;
+      } else {
+        const int n = (int)cur;
+        const float e = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(E[n >> 6]), n & 63));
+        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X[n >> 6]), n & 63));
+        if (!(fminf(tmax, x) <= e)) {
+          const unsigned ch = (unsigned)__builtin_amdgcn_readlane((int)CH[n >> 6], n & 63);
+          const uint32_t l = ch & 0xffffu, r = ch >> 16;
+          if (l & kLeafBit) {
+            const int si = (int)(l & 0x7fffu);
+            const float rl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(R[si >> 6]), si & 63));
+            if (!(rl <= tmin || rl >= tmax)) tmax = rl, hit = si;
+            if (r != 0xffffu) {
+              cur = r;
+              continue;  // a right leaf is tested by the next iteration, a right node visited
+            }
+          } else {
+            if (r != 0xffffu) ustack[sp++ * kBlock] = (uint16_t)r;
+            cur = l;
+            continue;
+          }
+        }
+      }
+      if (sp == 0) break;
+      cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)ustack[--sp * kBlock]);
+    }
+  }
+  out_tmax = tmax;
+  out_hit = hit;
+}
+
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
-constexpr int kNumStats = 22;
+constexpr int kNumStats = 25;
 constexpr int kSteps = 4;
 
 // kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
@@ -643,13 +870,20 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   float4 *nodes3 = (float4 *)lds;
   float4 *sph = nodes3 + (kLds ? 2 * V.n_nodes : 0);
   uint16_t *stack_base = (uint16_t *)(sph + (kLds ? V.n_spheres : 0));
+  float4 *nodes7 = (float4 *)lds;  // v7: Node7 records instead of nodes + spheres
+  if (kStep == 7) stack_base = (uint16_t *)(nodes7 + (kLds ? 4 * V.n_nodes7 : 0));
   if (kLds) {
-    for (int q = tid; q < 2 * V.n_nodes; q += kBlock) nodes3[q] = V.nodes_g[q];
-    for (int q = tid; q < V.n_spheres; q += kBlock) sph[q] = V.spheres_g[q];
+    if (kStep == 7) {
+      for (int q = tid; q < 4 * V.n_nodes7; q += kBlock) nodes7[q] = V.nodes7_g[q];
+    } else {
+      for (int q = tid; q < 2 * V.n_nodes; q += kBlock) nodes3[q] = V.nodes_g[q];
+      for (int q = tid; q < V.n_spheres; q += kBlock) sph[q] = V.spheres_g[q];
+    }
     __syncthreads();
   } else {
     nodes3 = (float4 *)V.nodes_g;
     sph = (float4 *)V.spheres_g;
+    nodes7 = (float4 *)V.nodes7_g;
   }
   uint16_t *stack = stack_base + tid;
   const int glane = blockIdx.x * kBlock + tid;
@@ -670,7 +904,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   //        executions of the sphere code, 15 (v5) wave-level executions of the fallback,
   //        16/17 clock64 / wall_clock64 ticks over the wave's lifetime (lane 0), 18/19 earliest
   //        wave start / latest wave end, 20 latest wave start, 21 first time the pixel counter ran
-  //        dry (wall_clock64; the host presets 18 and 21 to ~0)
+  //        dry (wall_clock64; the host presets 18 and 21 to ~0), 22 (v5) box tests that hit,
+  //        23 cooperative traces, 24 clocks in cooperative traces (lane 0)
   unsigned long long st[kNumStats] = {};
   long long t_iter = kStats ? (long long)clock64() : 0;
   const long long t_start = t_iter, w_start = kStats ? (long long)wall_clock64() : 0;
@@ -708,7 +943,21 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
     const int batch = min(V.shade_batch, (3 * live + 3) / 4);
-    const bool do_trav = trav != 0 && (int)__popcll(wait) < batch;
+    const bool coop = kStep == 5 && kLds && trav != 0 && live <= V.coop_lanes && __ballot(mode == kExit) != 0;
+    if (coop) {  // the frame's tail: trace each remaining ray with the whole wave
+      uint16_t *ustack = stack_base + (tid & ~63);
+      const long long c0 = kStats ? (long long)clock64() : 0;
+      for (uint64_t m = trav; m != 0; m &= m - 1) {
+        const int src = __builtin_ctzll(m);
+        float t;
+        int h;
+        coop_trace(V, nodes3, sph, ustack, L, src, tmin, t, h);
+        if (lane == src) L.tmax = t, L.hit = h, mode = kWait;
+        if (kStats && lane == 0) st[23]++;
+      }
+      if (kStats && lane == 0) st[24] += (long long)clock64() - c0;
+    }
+    const bool do_trav = !coop && trav != 0 && (int)__popcll(wait) < batch;
     if (kStats) last_kind = do_trav ? 0 : 1;
     if (do_trav) {
       // ---------------- traversal steps for every lane still traversing
@@ -741,8 +990,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
               px_steps++;
               if (L.cur & kLeafBit) st[6]++; else st[5]++;
             }
-            const bool done = kStep == 5 ? trav_step_v5<kStats>(V, nodes3, sph, stack, L, tmin, st)
-                                         : trav_step(V, nodes3, sph, stack, L, tmin);
+            const bool done = kStep == 7   ? trav_step_v7<kStats>(V, nodes7, stack, L, tmin, st)
+                              : kStep == 5 ? trav_step_v5<kStats>(V, nodes3, sph, stack, L, tmin, st)
+                                           : trav_step(V, nodes3, sph, stack, L, tmin);
             if (done) mode = kWait;
           }
       }
@@ -855,7 +1105,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     L.hit = -1;
     L.sp = 0;
     L.k = 0;
-    L.cur = V.root_items[0];
+    L.cur = kStep == 7 ? V.root7_items[0] : V.root_items[0];
     L.pend0 = L.pend1 = 0xffffu;
     have_result = true;
     if (kStats) st[4]++;
@@ -867,6 +1117,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       st[17] = (long long)wall_clock64() - w_start;
     }
     for (int q = 0; q < 18; q++) atomicAdd(&V.stats[q], st[q]);
+    atomicAdd(&V.stats[22], st[22]);
+    atomicAdd(&V.stats[23], st[23]);
+    atomicAdd(&V.stats[24], st[24]);
     if (lane == 0) {  // 18/19: earliest wave start, latest wave end (wall_clock64 ticks)
       atomicMin(&V.stats[18], (unsigned long long)w_start);
       atomicMax(&V.stats[19], (unsigned long long)wall_clock64());

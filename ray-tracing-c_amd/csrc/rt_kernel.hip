@@ -296,6 +296,7 @@ static bool book1_eligible(const rt_flat_scene *s) {
   if (s->n_lists != 2 || s->n_quads || s->n_translates || s->n_rotates || s->n_media) return false;  // root + lights
   if (s->lists[s->lights].count != 0) return false;
   if (s->n_spheres >= 0x7fff || s->n_bvh >= 0x7fff || s->camera.max_depth > kMaxDepth) return false;
+  if (s->n_bvh + s->lists[rt_ref_index(s->root)].count + 1 >= (int)b1::kHasLeaf7) return false;  // v7 refs
   for (int k = 0; k < s->n_materials; k++) {
     const rt_material &m = s->materials[k];
     if (m.tag != RT_MAT_LAMBERTIAN && m.tag != RT_MAT_METAL && m.tag != RT_MAT_DIELECTRIC) return false;
@@ -325,6 +326,55 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     pack_ref(n.right, &r);
     nodes[2 * k] = make_float4(n.lo[0], n.hi[0], n.lo[1], n.hi[1]);  // the reference's AABB values[axis][lo/hi]
     nodes[2 * k + 1] = make_float4(n.lo[2], n.hi[2], bits_as_float(l), bits_as_float(r));
+  }
+  // v7 records (rt_book1.h: Node7): own box + child refs, then the leaf children's spheres as
+  // (left, right) pairs; a sphere directly in the root list gets a record with an infinite box
+  std::vector<float4> nodes7;
+  std::vector<uint16_t> roots7;
+  {
+    auto has_leaf = [&](int node) {
+      return rt_ref_kind(s->bvh[node].left) == RT_KIND_SPHERE || rt_ref_kind(s->bvh[node].right) == RT_KIND_SPHERE;
+    };
+    auto ref7 = [&](int32_t ref) -> uint32_t {
+      if (ref == RT_REF_NONE) return 0xffffu;
+      const int32_t i = rt_ref_index(ref);
+      if (rt_ref_kind(ref) == RT_KIND_SPHERE) return (uint32_t)i | b1::kLeafBit;
+      return (uint32_t)i | (has_leaf(i) ? b1::kHasLeaf7 : 0u);
+    };
+    auto sphere_of = [&](int32_t ref, float *c, float *r2) {
+      if (ref != RT_REF_NONE && rt_ref_kind(ref) == RT_KIND_SPHERE) {
+        const rt_sphere &sp = s->spheres[rt_ref_index(ref)];
+        c[0] = sp.center[0], c[1] = sp.center[1], c[2] = sp.center[2], *r2 = sp.radius_sq;
+      } else {
+        c[0] = c[1] = c[2] = 0.0f, *r2 = 0.0f;
+      }
+    };
+    auto push_record = [&](const float lo[3], const float hi[3], int32_t left, int32_t right, uint32_t l, uint32_t r) {
+      float cl[3], cr[3], rl, rr;
+      sphere_of(left, cl, &rl);
+      sphere_of(right, cr, &rr);
+      nodes7.push_back(make_float4(lo[0], hi[0], lo[1], hi[1]));
+      nodes7.push_back(make_float4(lo[2], hi[2], bits_as_float(l), bits_as_float(r)));
+      nodes7.push_back(make_float4(cl[0], cr[0], cl[1], cr[1]));
+      nodes7.push_back(make_float4(cl[2], cr[2], rl, rr));
+    };
+    for (int k = 0; k < s->n_bvh; k++) {
+      const rt_bvh_node &n = s->bvh[k];
+      push_record(n.lo, n.hi, n.left, n.right, ref7(n.left), ref7(n.right));
+    }
+    const float inf = __builtin_inff(), lo_inf[3] = {-inf, -inf, -inf}, hi_inf[3] = {inf, inf, inf};
+    for (int k = 0; k < root.count; k++) {
+      const int32_t item = s->list_items[root.first + k];
+      if (rt_ref_kind(item) == RT_KIND_BVH) {
+        roots7.push_back((uint16_t)ref7(item));
+      } else {  // Sphere_hit straight from the list == an always-hit box around it (rt_book1.h)
+        roots7.push_back((uint16_t)((nodes7.size() / 4) | b1::kHasLeaf7));
+        push_record(lo_inf, hi_inf, item, RT_REF_NONE, ref7(item), 0xffffu);
+      }
+    }
+    if (roots7.empty()) roots7.push_back(0);
+    const float zero[3] = {0.0f, 0.0f, 0.0f};
+    push_record(zero, zero, RT_REF_NONE, RT_REF_NONE, 0xffffu, 0xffffu);  // the dummy record (no leaf children)
   }
   std::vector<float4> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++)
@@ -358,12 +408,14 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   }
 
   // geometry: LDS-resident when it fits next to the stack (gfx950: 160 KiB per CU)
-  const size_t scene_bytes = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
+  const size_t scene_bytes_v5 = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
+  const size_t scene_bytes_v7 = nodes7.size() * sizeof(float4);
   {
     const char *ev = getenv("RT_BOOK1_V");
     d->book1_ver = (ev && *ev) ? atoi(ev) : 5;
-    if (d->book1_ver != 2 && d->book1_ver != 3 && d->book1_ver != 6) d->book1_ver = 5;
+    if (d->book1_ver != 2 && d->book1_ver != 3 && d->book1_ver != 6 && d->book1_ver != 7) d->book1_ver = 5;
   }
+  const size_t scene_bytes = d->book1_ver == 7 ? scene_bytes_v7 : scene_bytes_v5;
   // v2 keeps 32-bit stack slots, v3+ 16-bit ones (+1 slot: v5+ store the right child unconditionally)
   // only the slots this scene's DFS can reach (host-computed `need` <= kStackSlots) take LDS
   const size_t stack_bytes = (size_t)(need + 1) * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
@@ -379,10 +431,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     d->book1_occ = (eo && *eo) ? atoi(eo) : 0;
     if (d->book1_ver != 5 || d->book1_stats || (d->book1_occ != 5 && d->book1_occ != 6)) d->book1_occ = 0;
   }
-  const void *fn = d->book1_stats ? (d->book1_ver == 6 ? (const void *)rt_book1_kernel<true, 6, true>
-                                                       : (const void *)rt_book1_kernel<true, 5, true>)
+  const void *fn = d->book1_stats ? (d->book1_ver == 6   ? (const void *)rt_book1_kernel<true, 6, true>
+                                     : d->book1_ver == 7 ? (const void *)rt_book1_kernel<true, 7, true>
+                                                         : (const void *)rt_book1_kernel<true, 5, true>)
                    : d->book1_occ == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 5> : (const void *)rt_book1_kernel<false, 5, false, 5>)
                    : d->book1_occ == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 6> : (const void *)rt_book1_kernel<false, 5, false, 6>)
+                   : d->book1_ver == 7 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 7> : (const void *)rt_book1_kernel<false, 7>)
                    : d->book1_ver == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 6> : (const void *)rt_book1_kernel<false, 6>)
                    : d->book1_ver == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>)
                    : d->book1_ver == 3 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 3> : (const void *)rt_book1_kernel<false, 3>)
@@ -393,11 +447,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth - b1::kRecRegs) * spill_lanes * sizeof(uint16_t);
 
-  size_t off[7], total = 0;
+  size_t off[9], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[7] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
-                           roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes};  // [4]: counter + stats
-  for (int k = 0; k < 7; k++) {
+  const size_t sizes[9] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+                           roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
+                           nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t)};
+  for (int k = 0; k < 9; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -408,6 +463,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   if (sizes[1]) HIP_OK(hipMemcpy(b + off[1], sph.data(), sizes[1], hipMemcpyHostToDevice));
   if (sizes[2]) HIP_OK(hipMemcpy(b + off[2], mats.data(), sizes[2], hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(b + off[3], roots.data(), sizes[3], hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b + off[7], nodes7.data(), sizes[7], hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(b + off[8], roots7.data(), sizes[8], hipMemcpyHostToDevice));
   d->b1_arena = arena;
   b1::Book1View &V = d->b1view;
   V.S = d->view;
@@ -419,6 +476,9 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.stats = (unsigned long long *)(b + off[4] + 64);
   V.spill = (uint16_t *)(b + off[5]);
   V.pixel_cost = d->book1_stats ? (uint32_t *)(b + off[6]) : nullptr;
+  V.nodes7_g = (const float4 *)(b + off[7]);
+  V.root7_items = (const uint16_t *)(b + off[8]);
+  V.n_nodes7 = (int32_t)(nodes7.size() / 4);
   V.spill_lanes = spill_lanes;
   V.n_nodes = s->n_bvh;
   V.n_spheres = s->n_spheres;
@@ -428,6 +488,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     const char *eb = getenv("RT_SHADE_BATCH");
     V.shade_batch = (eb && *eb) ? atoi(eb) : 48;
     V.shade_batch = V.shade_batch < 1 ? 1 : (V.shade_batch > 64 ? 64 : V.shade_batch);  // >= 1: progress
+    const char *ex = getenv("RT_EXPERIMENT");
+    V.experiment = (ex && *ex && d->book1_stats) ? atoi(ex) : 0;
+    const char *ec = getenv("RT_COOP_LANES");
+    V.coop_lanes = (ec && *ec) ? atoi(ec) : 0;  // off: measured slower than the DFS lanes
+    if (s->n_bvh > 64 * b1::kCoopSlots || s->n_spheres > 64 * b1::kCoopSlots || !d->book1_lds) V.coop_lanes = 0;
     const char *eo = getenv("RT_PIXEL_ORDER");
     V.reverse = (eo && !strcmp(eo, "rev")) ? 1 : 0;
     const char *es = getenv("RT_SPHERE_BATCH");
@@ -435,6 +500,10 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     V.sphere_batch = V.sphere_batch < 1 ? 1 : (V.sphere_batch > 64 ? 64 : V.sphere_batch);
   }
   d->book1 = true;
+  if (env_flag("RT_DEBUG", false))
+    fprintf(stderr, "[rtc] book1 v%d%s lds=%d bytes=%zu grid=%d (%d/CU) stack_need=%d occ=%d shade_batch=%d coop=%d\n",
+            d->book1_ver, d->book1_stats ? "+stats" : "", (int)d->book1_lds, d->b1_lds_bytes, d->b1_grid, per_cu, need,
+            d->book1_occ, V.shade_batch, V.coop_lanes);
   return 0;
 }
 
@@ -543,6 +612,9 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       case 600 + 5 * 4 + 0: RT_B1_LAUNCH(false, 5, false, 6); break;
       case 6 * 4 + 3: RT_B1_LAUNCH(true, 6, true); break;
       case 5 * 4 + 3: RT_B1_LAUNCH(true, 5, true); break;
+      case 7 * 4 + 1: RT_B1_LAUNCH(true, 7, false); break;
+      case 7 * 4 + 0: RT_B1_LAUNCH(false, 7, false); break;
+      case 7 * 4 + 3: RT_B1_LAUNCH(true, 7, true); break;
       case 6 * 4 + 1: RT_B1_LAUNCH(true, 6, false); break;
       case 6 * 4 + 0: RT_B1_LAUNCH(false, 6, false); break;
       case 5 * 4 + 1: RT_B1_LAUNCH(true, 5, false); break;
