@@ -127,6 +127,7 @@ def main():
     W, H, spp = sc.width, sc.height, sc.spp
     row0, stride, n_rows = rtc.rows_of(H, rank, world)
     ds = rtc.DeviceScene(sc, local)
+    kernel_name = ds.kernel_name
     buf = torch.zeros((max(n_rows, 1), W, 3), dtype=torch.uint8, device=f"cuda:{local}")
     stream = torch.cuda.current_stream(local)
 
@@ -209,16 +210,17 @@ def main():
             "data": "synthetic: the reference's procedural scene (pcg32 seed 19,29) and per-pixel pcg32 streams",
             "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "max_depth": args.depth, "partition": f"rows j % {world}", "rows_on_rank0": n_rows},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 4) if achieved else None,
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 4) if achieved else None,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 5) if achieved else None,
                          "traffic": traffic_for(config_key),
-                         "kernel": "rt_render_rows_kernel", "kernel_ms_avg": round(kernel_ms, 3),
+                         "kernel": kernel_name, "kernel_ms_avg": round(kernel_ms, 3),
                          "kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
                          "algorithmic_work": f"{ops:.0f} FP32 ops/sample (SURVEY §8d) x {launch_samples} samples/launch"
                          if ops else None,
-                         "note": "branchy FP32 VALU + u64 integer work, no MFMA; scene is L1/L2 resident, so the "
-                                 "HBM roof does not apply; peak = FP32 vector (= f32 MFMA) rate"},
+                         "note": "compute roof: the dense f32 peak (f32 MFMA rate = FP32 vector rate); the kernel is "
+                                 "branchy FP32 VALU + u64 integer work, no MFMA; the scene sits in LDS, so the HBM roof "
+                                 "does not apply; achieved counts the algorithmic FP32 ops only"},
             "cpu_baseline": base,
             "parity": parity,
         }

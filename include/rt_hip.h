@@ -67,7 +67,8 @@ int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int de
  * root-leaf steps, idle-in-shade iterations, shader clocks in traversal / shading iterations,
  * wave-level traversal / shading iterations, v6 wave-level box / sphere phases or v5 fast / fallback sphere tests, v5 wave-level sphere-code
  * and fallback executions, clock64 / wall_clock64 ticks of the waves' lifetimes, earliest start / latest end,
- * latest start, first pixel-counter exhaustion (wall_clock64), v5 box hits, cooperative traces and their clocks; n <= 25). */
+ * latest start, first pixel-counter exhaustion (wall_clock64), v5 box hits, cooperative traces and their clocks, v9 cooperative windows and scan steps;
+ * n <= 27). */
 int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out, int n);
 /* Diagnostics (same stats build): per work item of the last launch, {traversal steps, duration in
  * wall_clock64 ticks (100 MHz)} as 2 x uint32 each, for the first n_items items. */
@@ -78,6 +79,9 @@ int rt_book1_pixel_cost(rt_device_scene *dscene, uint32_t *out, int64_t n_items)
  * fn 1: division on `count` hashed pairs, fn 2: the sphere-hit outcome on hashed rays);
  * *mismatches receives the number of differing results. */
 int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches, int device);
+
+/* Name of the kernel rt_render_rows_async launches for `dscene` (as rocprofv3 lists it). */
+const char *rt_scene_kernel(const rt_device_scene *dscene);
 
 const char *rt_last_error(void);
 int rt_abi_version(void);

@@ -58,6 +58,8 @@ struct Book1View {
   const float4 *nodes7_g;    // v7: 4 float4 per record (Node7 below), then one all-zero dummy record
   const uint16_t *root7_items;
   int32_t n_nodes7;          // records incl. the dummy
+  const float4 *items9_g;    // v9: the world in traversal preorder, 2 float4 per item (Item9 below)
+  int32_t n_items9, n_items9_alloc;  // items, and items incl. the zero pad item at the end
   int32_t spill_lanes;
 };
 
@@ -464,9 +466,14 @@ RT_D float div_core(float x, float a, float ra) {  // == x / a for a in [kDivLo,
 // Sphere_hit (src/hittable.c:125-150) with the exact cores; lanes outside their ranges (NaN,
 // huge numerators, tiny discriminants, degenerate rays) evaluate the reference expression.
 template <bool kStats = false>
+RT_D void sphere_test_data(float4 s, int idx, Lane &L, float tmin, unsigned long long *st = nullptr);
+template <bool kStats = false>
 RT_D void sphere_test_v5(const float4 *sph, uint32_t ref, Lane &L, float tmin, unsigned long long *st = nullptr) {
   const int idx = (int)(ref & 0x7fff);
-  const float4 s = sph[idx];
+  sphere_test_data<kStats>(sph[idx], idx, L, tmin, st);
+}
+template <bool kStats>
+RT_D void sphere_test_data(float4 s, int idx, Lane &L, float tmin, unsigned long long *st) {
   const f3 oc = sub(mk(L.ox, L.oy, L.oz), mk(s.x, s.y, s.z));
   const float b = dot(oc, mk(L.dx, L.dy, L.dz));
   const float c = dot(oc, oc) - s.w;
@@ -689,6 +696,40 @@ RT_D bool trav_step_v7(const Book1View &V, const float4 *nodes7, uint16_t *stack
   return true;
 }
 
+// ---------------------------------------------------------------- v9: stackless preorder traversal
+// The reference's closest-hit recursion (HittableList_hit over the root items, BVHNode_hit = own box,
+// then left, then right: src/hittable.c:74-88, :266-277) visits the hittables in the preorder of the
+// world graph, skipping a node's whole subtree when its box misses.  v9 stores that preorder as a
+// flat item array, so the traversal is a scan with skips -- no stack, one item per step:
+//   node item:  q0 = (lo.x, hi.x, lo.y, hi.y), q1 = (lo.z, hi.z, skip, 0)   next = hit ? p+1 : p+skip
+//   leaf item:  q0 = (cx, cy, cz, r^2),        q1 = (-, -, -, idx | 1<<31)   Sphere_hit, next = p+1
+// (skip = 1 + the node's subtree size in items).  The box test sees exactly the reference's t_max:
+// every item before p in preorder that the reference would test has been tested, in order.
+constexpr uint32_t kLeaf9 = 0x80000000u;
+
+template <bool kStats = false>
+RT_D bool trav_step_v9(const Book1View &V, const float4 *items, Lane &L, float tmin, unsigned long long *st = nullptr) {
+  const uint32_t p = L.cur;
+  float4 q0 = items[2 * p], q1 = items[2 * p + 1];
+  // both halves in one LDS round trip: without this the compiler sinks the q1.xy / q1.z reads into
+  // the branches that use them, i.e. three dependent round trips per step.  (Reading the successor
+  // one step ahead measured slower: its moves and the re-read after a skip cost more than the latency.)
+  asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z), "+v"(q1.w));
+  const uint32_t w = __float_as_uint(q1.w);
+  uint32_t next = p + 1;
+  if (w & kLeaf9) {
+    if (kStats) st[6]++;
+    sphere_test_data<kStats>(q0, (int)(w & 0x7fffffffu), L, tmin, st);
+  } else {
+    if (kStats) st[5]++;
+    const bool hit = aabb_packed(q0, q1, L, tmin);
+    if (kStats && hit) st[22]++;
+    if (!hit) next = p + __float_as_uint(q1.z);
+  }
+  L.cur = next;
+  return next >= (uint32_t)V.n_items9;
+}
+
 // ---------------------------------------------------------------- v6: box and sphere phases
 // v5 tests the leaf spheres of a node inside the node's step, so every wave step runs the box code
 // AND two sphere tests whenever any lane of the wave has a leaf -- with a few lanes active in the
@@ -855,8 +896,67 @@ RT_D void coop_trace(const Book1View &V, const float4 *nodes3, const float4 *sph
   out_hit = hit;
 }
 
+// v9 form of the cooperative trace: the preorder scan itself is the walk.  The wave evaluates a
+// window of 64 consecutive items (box interval or sphere root, both t_max-independent), then scans
+// it with wave-uniform decisions; a skip past the window, or its end, starts the next window.
+template <bool kStats = false>
+RT_D void coop_trace9(const Book1View &V, const float4 *items, const Lane &L, int src, float tmin,
+                      float &out_tmax, int &out_hit, unsigned long long *st = nullptr) {
+  const int lane = __lane_id();
+  CoopRay C;
+  C.ox = lane_bcast(L.ox, src), C.oy = lane_bcast(L.oy, src), C.oz = lane_bcast(L.oz, src);
+  C.dx = lane_bcast(L.dx, src), C.dy = lane_bcast(L.dy, src), C.dz = lane_bcast(L.dz, src);
+  C.ix = lane_bcast(L.ix, src), C.iy = lane_bcast(L.iy, src), C.iz = lane_bcast(L.iz, src);
+  C.a = lane_bcast(L.a, src), C.ra = lane_bcast(L.ra, src);
+  C.fast = __builtin_amdgcn_readlane((int)L.fast, src) != 0;
+  const int n = V.n_items9;
+  float tmax = __builtin_inff();
+  int hit = -1;
+  int p = 0;
+  while (p < n) {
+    const int base = p;
+    const int q = base + lane;
+    if (kStats && lane == 0) st[25]++;
+    float v0 = 0.0f, v1 = 0.0f;  // node: E, X; leaf: root
+    uint32_t meta = 0;           // node: skip; leaf: index | kLeaf9
+    if (q < n) {
+      const float4 q0 = items[2 * q], q1 = items[2 * q + 1];
+      meta = __float_as_uint(q1.w);
+      if (meta & kLeaf9) {
+        v0 = coop_sphere_root(q0, C, tmin);
+      } else {
+        const float t0x = (q0.x - C.ox) * C.ix, t1x = (q0.y - C.ox) * C.ix;
+        const float t0y = (q0.z - C.oy) * C.iy, t1y = (q0.w - C.oy) * C.iy;
+        const float t0z = (q1.x - C.oz) * C.iz, t1z = (q1.y - C.oz) * C.iz;
+        const float nx = C.ix < 0 ? t1x : t0x, fx = C.ix < 0 ? t0x : t1x;
+        const float ny = C.iy < 0 ? t1y : t0y, fy = C.iy < 0 ? t0y : t1y;
+        const float nz = C.iz < 0 ? t1z : t0z, fz = C.iz < 0 ? t0z : t1z;
+        v0 = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+        v1 = fminf(fminf(fx, fy), fz);
+        meta = __float_as_uint(q1.z);
+      }
+    }
+    const int end = min(n, base + 64);
+    while (p < end) {
+      if (kStats && lane == 0) st[26]++;
+      const int l = p - base;
+      const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, l);
+      const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0), l));
+      if (m & kLeaf9) {
+        if (!(a <= tmin || a >= tmax)) tmax = a, hit = (int)(m & 0x7fffffffu);
+        p++;
+      } else {
+        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v1), l));
+        p += !(fminf(tmax, x) <= a) ? 1 : (int)m;
+      }
+    }
+  }
+  out_tmax = tmax;
+  out_hit = hit;
+}
+
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
-constexpr int kNumStats = 25;
+constexpr int kNumStats = 27;
 constexpr int kSteps = 4;
 
 // kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
@@ -871,10 +971,14 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   float4 *sph = nodes3 + (kLds ? 2 * V.n_nodes : 0);
   uint16_t *stack_base = (uint16_t *)(sph + (kLds ? V.n_spheres : 0));
   float4 *nodes7 = (float4 *)lds;  // v7: Node7 records instead of nodes + spheres
+  float4 *items9 = (float4 *)lds;  // v9: preorder items, no stack
   if (kStep == 7) stack_base = (uint16_t *)(nodes7 + (kLds ? 4 * V.n_nodes7 : 0));
+  if (kStep == 9) stack_base = (uint16_t *)(items9 + (kLds ? 2 * V.n_items9_alloc : 0));
   if (kLds) {
     if (kStep == 7) {
       for (int q = tid; q < 4 * V.n_nodes7; q += kBlock) nodes7[q] = V.nodes7_g[q];
+    } else if (kStep == 9) {
+      for (int q = tid; q < 2 * V.n_items9_alloc; q += kBlock) items9[q] = V.items9_g[q];
     } else {
       for (int q = tid; q < 2 * V.n_nodes; q += kBlock) nodes3[q] = V.nodes_g[q];
       for (int q = tid; q < V.n_spheres; q += kBlock) sph[q] = V.spheres_g[q];
@@ -884,6 +988,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     nodes3 = (float4 *)V.nodes_g;
     sph = (float4 *)V.spheres_g;
     nodes7 = (float4 *)V.nodes7_g;
+    items9 = (float4 *)V.items9_g;
   }
   uint16_t *stack = stack_base + tid;
   const int glane = blockIdx.x * kBlock + tid;
@@ -905,7 +1010,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   //        16/17 clock64 / wall_clock64 ticks over the wave's lifetime (lane 0), 18/19 earliest
   //        wave start / latest wave end, 20 latest wave start, 21 first time the pixel counter ran
   //        dry (wall_clock64; the host presets 18 and 21 to ~0), 22 (v5) box tests that hit,
-  //        23 cooperative traces, 24 clocks in cooperative traces (lane 0)
+  //        23 cooperative traces, 24 clocks in cooperative traces (lane 0), 25/26 (v9) cooperative
+  //        windows / scan steps
   unsigned long long st[kNumStats] = {};
   long long t_iter = kStats ? (long long)clock64() : 0;
   const long long t_start = t_iter, w_start = kStats ? (long long)wall_clock64() : 0;
@@ -943,7 +1049,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
     const int batch = min(V.shade_batch, (3 * live + 3) / 4);
-    const bool coop = kStep == 5 && kLds && trav != 0 && live <= V.coop_lanes && __ballot(mode == kExit) != 0;
+    const bool coop = (kStep == 5 || kStep == 9) && kLds && trav != 0 && live <= V.coop_lanes &&
+                      __ballot(mode == kExit) != 0;
     if (coop) {  // the frame's tail: trace each remaining ray with the whole wave
       uint16_t *ustack = stack_base + (tid & ~63);
       const long long c0 = kStats ? (long long)clock64() : 0;
@@ -951,7 +1058,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const int src = __builtin_ctzll(m);
         float t;
         int h;
-        coop_trace(V, nodes3, sph, ustack, L, src, tmin, t, h);
+        if (kStep == 9)
+          coop_trace9<kStats>(V, items9, L, src, tmin, t, h, st);
+        else
+          coop_trace(V, nodes3, sph, ustack, L, src, tmin, t, h);
         if (lane == src) L.tmax = t, L.hit = h, mode = kWait;
         if (kStats && lane == 0) st[23]++;
       }
@@ -988,9 +1098,12 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
             if (kStats) {
               st[1]++;
               px_steps++;
-              if (L.cur & kLeafBit) st[6]++; else st[5]++;
+              if (kStep != 9) {
+                if (L.cur & kLeafBit) st[6]++; else st[5]++;
+              }
             }
-            const bool done = kStep == 7   ? trav_step_v7<kStats>(V, nodes7, stack, L, tmin, st)
+            const bool done = kStep == 9   ? trav_step_v9<kStats>(V, items9, L, tmin, st)
+                              : kStep == 7 ? trav_step_v7<kStats>(V, nodes7, stack, L, tmin, st)
                               : kStep == 5 ? trav_step_v5<kStats>(V, nodes3, sph, stack, L, tmin, st)
                                            : trav_step(V, nodes3, sph, stack, L, tmin);
             if (done) mode = kWait;
@@ -1105,11 +1218,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     L.hit = -1;
     L.sp = 0;
     L.k = 0;
-    L.cur = kStep == 7 ? V.root7_items[0] : V.root_items[0];
+    L.cur = kStep == 9 ? 0u : kStep == 7 ? V.root7_items[0] : V.root_items[0];
     L.pend0 = L.pend1 = 0xffffu;
     have_result = true;
     if (kStats) st[4]++;
-    mode = V.n_root > 0 ? kTrav : kWait;
+    mode = (kStep == 9 ? V.n_items9 : V.n_root) > 0 ? kTrav : kWait;
   }
   if (kStats) {
     if (lane == 0) {  // 16/17: clock64 and wall_clock64 (100 MHz) ticks over the wave's lifetime
@@ -1120,6 +1233,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     atomicAdd(&V.stats[22], st[22]);
     atomicAdd(&V.stats[23], st[23]);
     atomicAdd(&V.stats[24], st[24]);
+    atomicAdd(&V.stats[25], st[25]);
+    atomicAdd(&V.stats[26], st[26]);
     if (lane == 0) {  // 18/19: earliest wave start, latest wave end (wall_clock64 ticks)
       atomicMin(&V.stats[18], (unsigned long long)w_start);
       atomicMax(&V.stats[19], (unsigned long long)wall_clock64());

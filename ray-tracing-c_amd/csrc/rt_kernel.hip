@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <functional>
 #include <vector>
 
 #include "../../include/rt_hip.h"
@@ -167,7 +168,7 @@ struct rt_device_scene {
   // Book-1 fast path (rt_book1.h), when the scene qualifies
   bool book1 = false;
   bool book1_lds = false;
-  int book1_ver = 5;
+  int book1_ver = 9;
   int book1_occ = 0;         // register-allocation occupancy target of the launched variant (0: default)
   bool book1_stats = false;  // diagnostic counters build (RT_BOOK1_STATS=1)
   b1::Book1View b1view;
@@ -376,6 +377,31 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     const float zero[3] = {0.0f, 0.0f, 0.0f};
     push_record(zero, zero, RT_REF_NONE, RT_REF_NONE, 0xffffu, 0xffffu);  // the dummy record (no leaf children)
   }
+  // v9 items (rt_book1.h: trav_step_v9): the root list's hittables in traversal preorder
+  std::vector<float4> items9;
+  {
+    std::function<void(int32_t)> emit = [&](int32_t ref) {
+      if (ref == RT_REF_NONE) return;
+      const int32_t i = rt_ref_index(ref);
+      if (rt_ref_kind(ref) == RT_KIND_SPHERE) {
+        const rt_sphere &sp = s->spheres[i];
+        items9.push_back(make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius_sq));
+        items9.push_back(make_float4(0.0f, 0.0f, 0.0f, bits_as_float((uint32_t)i | b1::kLeaf9)));
+        return;
+      }
+      const rt_bvh_node &n = s->bvh[i];
+      const size_t at = items9.size();
+      items9.push_back(make_float4(n.lo[0], n.hi[0], n.lo[1], n.hi[1]));
+      items9.push_back(make_float4(n.lo[2], n.hi[2], 0.0f, 0.0f));
+      emit(n.left);
+      emit(n.right);  // RT_REF_NONE for the collapsed n == 1 duplicate (rt_flatten.c)
+      items9[at + 1].z = bits_as_float((uint32_t)((items9.size() - at) / 2));
+    };
+    for (int k = 0; k < root.count; k++) emit(s->list_items[root.first + k]);
+    // one zero item past the end: the step reads its successor before knowing it exists
+    items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  }
   std::vector<float4> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++)
     sph[k] = make_float4(s->spheres[k].center[0], s->spheres[k].center[1], s->spheres[k].center[2],
@@ -410,15 +436,17 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   // geometry: LDS-resident when it fits next to the stack (gfx950: 160 KiB per CU)
   const size_t scene_bytes_v5 = nodes.size() * sizeof(float4) + sph.size() * sizeof(float4);
   const size_t scene_bytes_v7 = nodes7.size() * sizeof(float4);
+  const size_t scene_bytes_v9 = items9.size() * sizeof(float4);
   {
     const char *ev = getenv("RT_BOOK1_V");
-    d->book1_ver = (ev && *ev) ? atoi(ev) : 5;
-    if (d->book1_ver != 2 && d->book1_ver != 3 && d->book1_ver != 6 && d->book1_ver != 7) d->book1_ver = 5;
+    d->book1_ver = (ev && *ev) ? atoi(ev) : 9;
+    if (d->book1_ver != 2 && d->book1_ver != 3 && d->book1_ver != 5 && d->book1_ver != 6 && d->book1_ver != 7)
+      d->book1_ver = 9;
   }
-  const size_t scene_bytes = d->book1_ver == 7 ? scene_bytes_v7 : scene_bytes_v5;
+  const size_t scene_bytes = d->book1_ver == 9 ? scene_bytes_v9 : d->book1_ver == 7 ? scene_bytes_v7 : scene_bytes_v5;
   // v2 keeps 32-bit stack slots, v3+ 16-bit ones (+1 slot: v5+ store the right child unconditionally)
   // only the slots this scene's DFS can reach (host-computed `need` <= kStackSlots) take LDS
-  const size_t stack_bytes = (size_t)(need + 1) * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
+  const size_t stack_bytes = d->book1_ver == 9 ? 0 : (size_t)(need + 1) * b1::kBlock * (d->book1_ver >= 3 ? 2 : 4);
   d->book1_lds = env_flag("RT_BOOK1_LDS", true) && scene_bytes + stack_bytes <= 64 * 1024;
   d->book1_stats = env_flag("RT_BOOK1_STATS", false) && d->book1_ver >= 5 && d->book1_lds;
   d->b1_lds_bytes = align_up((d->book1_lds ? scene_bytes : 0) + stack_bytes, 16);
@@ -431,11 +459,13 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     d->book1_occ = (eo && *eo) ? atoi(eo) : 0;
     if (d->book1_ver != 5 || d->book1_stats || (d->book1_occ != 5 && d->book1_occ != 6)) d->book1_occ = 0;
   }
-  const void *fn = d->book1_stats ? (d->book1_ver == 6   ? (const void *)rt_book1_kernel<true, 6, true>
+  const void *fn = d->book1_stats ? (d->book1_ver == 9   ? (const void *)rt_book1_kernel<true, 9, true>
+                                     : d->book1_ver == 6 ? (const void *)rt_book1_kernel<true, 6, true>
                                      : d->book1_ver == 7 ? (const void *)rt_book1_kernel<true, 7, true>
                                                          : (const void *)rt_book1_kernel<true, 5, true>)
                    : d->book1_occ == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 5> : (const void *)rt_book1_kernel<false, 5, false, 5>)
                    : d->book1_occ == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5, false, 6> : (const void *)rt_book1_kernel<false, 5, false, 6>)
+                   : d->book1_ver == 9 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 9> : (const void *)rt_book1_kernel<false, 9>)
                    : d->book1_ver == 7 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 7> : (const void *)rt_book1_kernel<false, 7>)
                    : d->book1_ver == 6 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 6> : (const void *)rt_book1_kernel<false, 6>)
                    : d->book1_ver == 5 ? (d->book1_lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>)
@@ -447,12 +477,13 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth - b1::kRecRegs) * spill_lanes * sizeof(uint16_t);
 
-  size_t off[9], total = 0;
+  size_t off[10], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[9] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+  const size_t sizes[10] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
                            roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
-                           nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t)};
-  for (int k = 0; k < 9; k++) {
+                           nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t),
+                           items9.size() * sizeof(float4)};
+  for (int k = 0; k < 10; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -465,6 +496,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   HIP_OK(hipMemcpy(b + off[3], roots.data(), sizes[3], hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(b + off[7], nodes7.data(), sizes[7], hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(b + off[8], roots7.data(), sizes[8], hipMemcpyHostToDevice));
+  if (sizes[9]) HIP_OK(hipMemcpy(b + off[9], items9.data(), sizes[9], hipMemcpyHostToDevice));
   d->b1_arena = arena;
   b1::Book1View &V = d->b1view;
   V.S = d->view;
@@ -479,6 +511,9 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.nodes7_g = (const float4 *)(b + off[7]);
   V.root7_items = (const uint16_t *)(b + off[8]);
   V.n_nodes7 = (int32_t)(nodes7.size() / 4);
+  V.items9_g = (const float4 *)(b + off[9]);
+  V.n_items9 = (int32_t)(items9.size() / 2) - 1;  // without the trailing pad item
+  V.n_items9_alloc = (int32_t)(items9.size() / 2);
   V.spill_lanes = spill_lanes;
   V.n_nodes = s->n_bvh;
   V.n_spheres = s->n_spheres;
@@ -492,7 +527,9 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     V.experiment = (ex && *ex && d->book1_stats) ? atoi(ex) : 0;
     const char *ec = getenv("RT_COOP_LANES");
     V.coop_lanes = (ec && *ec) ? atoi(ec) : 0;  // off: measured slower than the DFS lanes
-    if (s->n_bvh > 64 * b1::kCoopSlots || s->n_spheres > 64 * b1::kCoopSlots || !d->book1_lds) V.coop_lanes = 0;
+    if ((d->book1_ver == 5 && (s->n_bvh > 64 * b1::kCoopSlots || s->n_spheres > 64 * b1::kCoopSlots)) ||
+        (d->book1_ver != 5 && d->book1_ver != 9) || !d->book1_lds)
+      V.coop_lanes = 0;
     const char *eo = getenv("RT_PIXEL_ORDER");
     V.reverse = (eo && !strcmp(eo, "rev")) ? 1 : 0;
     const char *es = getenv("RT_SPHERE_BATCH");
@@ -612,6 +649,9 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       case 600 + 5 * 4 + 0: RT_B1_LAUNCH(false, 5, false, 6); break;
       case 6 * 4 + 3: RT_B1_LAUNCH(true, 6, true); break;
       case 5 * 4 + 3: RT_B1_LAUNCH(true, 5, true); break;
+      case 9 * 4 + 1: RT_B1_LAUNCH(true, 9, false); break;
+      case 9 * 4 + 0: RT_B1_LAUNCH(false, 9, false); break;
+      case 9 * 4 + 3: RT_B1_LAUNCH(true, 9, true); break;
       case 7 * 4 + 1: RT_B1_LAUNCH(true, 7, false); break;
       case 7 * 4 + 0: RT_B1_LAUNCH(false, 7, false); break;
       case 7 * 4 + 3: RT_B1_LAUNCH(true, 7, true); break;
@@ -762,4 +802,16 @@ extern "C" int rt_book1_pixel_cost(rt_device_scene *d, uint32_t *out, int64_t n_
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemcpy(out, d->b1view.pixel_cost, (size_t)n_items * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return 0;
+}
+
+// Name of the kernel rt_render_rows_async launches for this scene (as rocprofv3 reports it).
+extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
+  static thread_local char buf[160];
+  if (!d) return "";
+  if (!d->book1)
+    snprintf(buf, sizeof buf, "rt_render_rows_kernel<%d>", (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll);
+  else
+    snprintf(buf, sizeof buf, "rt_book1_kernel<%s, %d, %s, %d>", d->book1_lds ? "true" : "false", d->book1_ver,
+             d->book1_stats ? "true" : "false", d->book1_occ);
+  return buf;
 }

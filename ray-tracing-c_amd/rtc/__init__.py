@@ -118,6 +118,8 @@ def lib() -> ctypes.CDLL:
         L.rt_diag_libm.restype = c_int
         L.rt_diag_arith.argtypes = [c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_int]
         L.rt_diag_arith.restype = c_int
+        L.rt_scene_kernel.argtypes = [c_void_p]
+        L.rt_scene_kernel.restype = c_char_p
         L.rt_last_error.restype = c_char_p
         L.rt_abi_version.restype = c_int
         _lib = L
@@ -217,6 +219,11 @@ class DeviceScene:
                                         c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
         if rc != 0:
             raise RtcError(f"rt_render_rows_async failed: {last_error()}")
+
+    @property
+    def kernel_name(self) -> str:
+        """The kernel rt_render_rows_async launches for this scene (rocprofv3's name for it)."""
+        return (lib().rt_scene_kernel(self._h) or b"").decode()
 
     def close(self):
         if self._h:
