@@ -12,7 +12,7 @@
 //    ([slot][lane], 16-bit refs: conflict-free); traversal keeps the reference's left-then-right
 //    order and shrinking t_max, tests leaf spheres inline, and never pushes the left child;
 //  * the path record is a list of material ids (albedo of a Solid texture is a function of the
-//    material) in registers (kRecRegs slots) + a per-lane global spill area for deep paths; the
+//    material) in registers (two 4-id chunks) + a per-lane global spill area for deep paths; the
 //    colour is folded innermost-first at path end exactly like the recursion.
 //
 // Eligibility (host-checked, rt_kernel.hip: book1_eligible): spheres only, BVH nodes, lists only at
@@ -26,7 +26,6 @@ namespace b1 {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kStackSlots = 16;   // per-lane DFS slots in LDS, 32-bit (host checks the need)
-constexpr int kRecRegs = 8;       // path-record slots held in registers (4 x 16-bit per u64)
 constexpr uint16_t kLeafBit = 0x8000;  // 16-bit ref: leaf sphere index | kLeafBit, else node index
 constexpr uint16_t kHasLeaf7 = 0x4000; // v7 node refs: the node has a leaf child (its record's spheres are read)
 
@@ -54,7 +53,7 @@ struct Book1View {
   int32_t experiment;        // stats builds only: timing experiments that change the image (RT_EXPERIMENT)
   unsigned long long *stats; // diagnostic counters (kStats builds only)
   uint32_t *pixel_cost;      // kStats: per work item {traversal steps, wall_clock64 ticks}
-  uint16_t *spill;           // [slot - kRecRegs][global lane] for deep paths
+  uint64_t *spill;           // [chunk][global lane]: a deep path's older 4-id chunks (Record)
   const float4 *nodes7_g;    // v7: 4 float4 per record (Node7 below), then one all-zero dummy record
   const uint16_t *root7_items;
   int32_t n_nodes7;          // records incl. the dummy
@@ -162,35 +161,40 @@ RT_D void trace(const Book1View &V, const float4 *nodes, const float4 *sph, uint
 }
 
 // ---------------------------------------------------------------- path record
+// The path's material ids in push order, in chunks of 4 (16 bits each, newest in the low bits):
+// r0 = the current chunk, r1 = the previous one; older chunks go to the per-lane spill area as one
+// u64 each (one 8-byte store per 4 bounces beyond the 8th, instead of a 2-byte store per bounce).
 struct Record {
-  uint64_t r0, r1;  // 8 x 16-bit material ids, newest in the low bits of r0
-  int n;
+  uint64_t r0, r1;
+  int n;  // ids pushed
 };
 
 RT_D void rec_push(const Book1View &V, Record &R, uint32_t id, int glane) {
-  if (R.n >= kRecRegs) {  // oldest register slot moves to the spill area (rare: deep paths)
-    const uint16_t oldest = (uint16_t)(R.r1 >> 48);
-    V.spill[(int64_t)(R.n - kRecRegs) * V.spill_lanes + glane] = oldest;
+  if ((R.n & 3) == 0 && R.n > 0) {  // r0 is a complete chunk: start a new one
+    if (R.n >= 8) V.spill[(int64_t)((R.n >> 2) - 2) * V.spill_lanes + glane] = R.r1;  // deep paths only
+    R.r1 = R.r0;
+    R.r0 = 0;
   }
-  R.r1 = (R.r1 << 16) | (R.r0 >> 48);
   R.r0 = (R.r0 << 16) | id;
   R.n++;
 }
 
 // c = a_k * c for k = n-1 .. 0 (newest first), the recursion's evaluation order
+RT_D f3 rec_fold_chunk(const Book1View &V, uint64_t w, int cnt, f3 c) {
+  for (int k = 0; k < cnt; k++) {
+    const FastMat &m = V.mats[(uint32_t)(w & 0xffff)];
+    c = add(mk(0.0f, 0.0f, 0.0f), mul(ld3(m.albedo), c));
+    w >>= 16;
+  }
+  return c;
+}
 RT_D f3 rec_fold(const Book1View &V, const Record &R, f3 c, int glane) {
-  uint64_t r0 = R.r0, r1 = R.r1;
-  const int in_regs = R.n < kRecRegs ? R.n : kRecRegs;
-  for (int k = 0; k < in_regs; k++) {
-    const FastMat &m = V.mats[(uint32_t)(r0 & 0xffff)];
-    c = add(mk(0.0f, 0.0f, 0.0f), mul(ld3(m.albedo), c));
-    r0 = (r0 >> 16) | (r1 << 48);
-    r1 >>= 16;
-  }
-  for (int k = R.n - kRecRegs - 1; k >= 0; k--) {
-    const FastMat &m = V.mats[V.spill[(int64_t)k * V.spill_lanes + glane]];
-    c = add(mk(0.0f, 0.0f, 0.0f), mul(ld3(m.albedo), c));
-  }
+  if (R.n == 0) return c;
+  const int cnt0 = R.n - (((R.n - 1) >> 2) << 2);  // ids in the current chunk, 1..4
+  c = rec_fold_chunk(V, R.r0, cnt0, c);
+  if (R.n > cnt0) c = rec_fold_chunk(V, R.r1, 4, c);
+  for (int q = ((R.n - 1) >> 2) - 2; q >= 0; q--)  // spilled chunks, newest first
+    c = rec_fold_chunk(V, V.spill[(int64_t)q * V.spill_lanes + glane], 4, c);
   return c;
 }
 

@@ -475,7 +475,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   if (per_cu < 1) per_cu = 1;
   d->b1_grid = prop.multiProcessorCount * per_cu;
   const int spill_lanes = d->b1_grid * b1::kBlock;
-  const size_t spill_bytes = (size_t)(kMaxDepth - b1::kRecRegs) * spill_lanes * sizeof(uint16_t);
+  const size_t spill_bytes = (size_t)(kMaxDepth / 4) * spill_lanes * sizeof(uint64_t);  // Record chunks
 
   size_t off[10], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
@@ -506,7 +506,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.root_items = (const uint16_t *)(b + off[3]);
   V.work_counter = (int32_t *)(b + off[4]);
   V.stats = (unsigned long long *)(b + off[4] + 64);
-  V.spill = (uint16_t *)(b + off[5]);
+  V.spill = (uint64_t *)(b + off[5]);
   V.pixel_cost = d->book1_stats ? (uint32_t *)(b + off[6]) : nullptr;
   V.nodes7_g = (const float4 *)(b + off[7]);
   V.root7_items = (const uint16_t *)(b + off[8]);
