@@ -44,7 +44,9 @@ void rt_scene_release(rt_device_scene *dscene);
 
 /* Render rows row0, row0 + row_stride, ... (n_rows of them) into d_out (device pointer,
  * n_rows * width * 3 bytes, compact, in that row order).  Asynchronous on `stream`
- * (hipStream_t, NULL = default stream of the scene's device).  This is the hot path. */
+ * (hipStream_t, NULL = default stream of the scene's device).  This is the hot path.
+ * Book-1 scenes at >= 32 spp first run a low-spp cost pass (RT_LPT_SPP, default 8; RT_LPT=0 turns
+ * it off) and hand out the pixels longest-first; the image does not depend on the order. */
 int rt_render_rows_async(rt_device_scene *dscene, int row0, int row_stride, int n_rows, uint8_t *d_out,
                          void *stream);
 
@@ -79,6 +81,11 @@ int rt_book1_pixel_cost(rt_device_scene *dscene, uint32_t *out, int64_t n_items)
  * fn 1: division on `count` hashed pairs, fn 2: the sphere-hit outcome on hashed rays);
  * *mismatches receives the number of differing results. */
 int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches, int device);
+
+/* Milliseconds of the last frame launch rt_render_rows_async made for `dscene` (HIP events on its
+ * stream; call after that work completed).  Excludes the longest-first cost pre-pass
+ * (rt_book1_cost_kernel, RT_LPT).  -1 when unavailable. */
+double rt_scene_last_launch_ms(rt_device_scene *dscene);
 
 /* Name of the kernel rt_render_rows_async launches for `dscene` (as rocprofv3 lists it). */
 const char *rt_scene_kernel(const rt_device_scene *dscene);

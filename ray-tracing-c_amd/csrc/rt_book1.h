@@ -49,6 +49,8 @@ struct Book1View {
   int32_t shade_batch;       // v3+: shade once this many lanes of a wave are waiting
   int32_t sphere_batch;      // v6: run a sphere phase once this many lanes have a pending sphere
   int32_t reverse;           // hand out work items last-first
+  const int32_t *order;      // work item order (longest-first from the cost pre-pass), or null
+  uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   int32_t coop_lanes;        // v5: cooperative traversal once the counter is dry and <= this many lanes live
   int32_t experiment;        // stats builds only: timing experiments that change the image (RT_EXPERIMENT)
   unsigned long long *stats; // diagnostic counters (kStats builds only)
@@ -1099,9 +1101,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #pragma unroll
         for (int u = 0; u < kSteps; u++)
           if (mode == kTrav) {
+            px_steps++;  // work-item cost (the LPT pre-pass, stats builds)
             if (kStats) {
               st[1]++;
-              px_steps++;
               if (kStep != 9) {
                 if (L.cur & kLeafBit) st[6]++; else st[5]++;
               }
@@ -1148,6 +1150,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         s++;
         if (s == spp) {  // quantize (src/raytracing.c:127-131)
           write_pixel(out + pix * 3, acc, spp);
+          if (V.cost_out) V.cost_out[pix] = px_steps;
           if (kStats) {
             V.pixel_cost[2 * pix] = px_steps;
             V.pixel_cost[2 * pix + 1] = (uint32_t)((long long)wall_clock64() - px_t0);
@@ -1171,7 +1174,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           mode = kExit;
           break;
         }
-        if (V.reverse) pix = total - 1 - pix;  // bottom rows (ground, spheres: long paths) first
+        if (V.order) pix = V.order[pix];  // longest work items first
+        else if (V.reverse) pix = total - 1 - pix;
         const int jj = (int)(pix / W);
         i = (int)(pix - (int64_t)jj * W);
         j = V.row0 + jj * V.row_stride;
@@ -1179,7 +1183,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         acc = mk(0.0f, 0.0f, 0.0f);
         s = 0;
         need_pixel = false;
-        if (kStats) px_steps = 0, px_t0 = (long long)wall_clock64();
+        px_steps = 0;
+        if (kStats) px_t0 = (long long)wall_clock64();
       }
       // camera ray (src/raytracing.c:96-122)
       const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));

@@ -71,6 +71,14 @@ __global__ __launch_bounds__(b1::kBlock, kOcc > 0 ? kOcc : 1) void rt_book1_kern
     b1::render<kLds>(V, out, lds);
 }
 
+// The LPT cost pre-pass: the same persistent kernel at low spp, under its own name so profiles
+// separate it from the frame's launch.
+template <bool kLds, int kVer>
+__global__ __launch_bounds__(b1::kBlock) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  b1::render_batched<kLds, false, kVer>(V, out, lds);
+}
+
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -157,6 +165,39 @@ __global__ void rt_diag_arith_kernel(int fn, uint64_t start, uint64_t count, uin
   if (bad) atomicAdd(mism, bad);
 }
 
+// Longest-first work order (rt_render_rows_async): bucket work items by log2(cost) with 3 mantissa
+// bits (256 buckets), highest bucket first.  Order inside a bucket is arbitrary (atomics): any order
+// renders the same image, the order only decides which pixels start first.
+__device__ __forceinline__ uint32_t lpt_bucket(uint32_t c) {
+  c |= 1u;
+  const int e = 31 - __clz(c);
+  const uint32_t frac = e >= 3 ? (c >> (e - 3)) & 7u : (c << (3 - e)) & 7u;
+  const uint32_t k = (uint32_t)e * 8u + frac;
+  return k > 255u ? 255u : k;
+}
+__global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist) {
+  __shared__ uint32_t h[256];
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicAdd(&h[lpt_bucket(cost[i])], 1u);
+  __syncthreads();
+  for (int k = threadIdx.x; k < 256; k += blockDim.x)
+    if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+__global__ void lpt_scan_kernel(uint32_t *hist) {  // one thread: offsets, highest bucket first
+  if (threadIdx.x != 0) return;
+  uint32_t run = 0;
+  for (int k = 255; k >= 0; k--) {
+    hist[256 + k] = run;
+    run += hist[k];
+  }
+}
+__global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
+}
+
 // ------------------------------------------------------------------------------ device scene
 struct rt_device_scene {
   int device;
@@ -173,6 +214,13 @@ struct rt_device_scene {
   bool book1_stats = false;  // diagnostic counters build (RT_BOOK1_STATS=1)
   b1::Book1View b1view;
   void *b1_arena = nullptr;
+  // longest-first work order from a low-spp cost pre-pass (RT_LPT, RT_LPT_SPP)
+  bool lpt = false;
+  int lpt_spp = 8;
+  uint32_t *lpt_cost = nullptr;  // steps per work item (W*H)
+  int32_t *lpt_order = nullptr;  // work item order (W*H)
+  uint32_t *lpt_hist = nullptr;  // 256 bucket counts + 256 running offsets
+  hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
   int b1_grid = 0;
   size_t b1_lds_bytes = 0;
 };
@@ -477,13 +525,16 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth / 4) * spill_lanes * sizeof(uint64_t);  // Record chunks
 
-  size_t off[10], total = 0;
+  size_t off[13], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[10] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+  const size_t sizes[13] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
                            roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
                            nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t),
-                           items9.size() * sizeof(float4)};
-  for (int k = 0; k < 10; k++) {
+                           items9.size() * sizeof(float4),
+                           (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
+                           (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
+                           512 * sizeof(uint32_t)};                                          // [12] LPT buckets
+  for (int k = 0; k < 13; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -512,6 +563,17 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.root7_items = (const uint16_t *)(b + off[8]);
   V.n_nodes7 = (int32_t)(nodes7.size() / 4);
   V.items9_g = (const float4 *)(b + off[9]);
+  d->lpt_cost = (uint32_t *)(b + off[10]);
+  d->lpt_order = (int32_t *)(b + off[11]);
+  d->lpt_hist = (uint32_t *)(b + off[12]);
+  d->lpt = env_flag("RT_LPT", true) && (d->book1_ver == 9 || d->book1_ver == 5) && d->book1_occ == 0;
+  {
+    const char *el = getenv("RT_LPT_SPP");
+    d->lpt_spp = (el && *el) ? atoi(el) : 8;
+    if (d->lpt_spp < 1) d->lpt_spp = 1;
+  }
+  V.order = nullptr;
+  V.cost_out = nullptr;
   V.n_items9 = (int32_t)(items9.size() / 2) - 1;  // without the trailing pad item
   V.n_items9_alloc = (int32_t)(items9.size() / 2);
   V.spill_lanes = spill_lanes;
@@ -603,6 +665,8 @@ extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) 
   const void *dev_arrays[13];
   for (int k = 0; k < 13; k++) dev_arrays[k] = (char *)arena + parts[k].off;
   d->view = make_view(*s, dev_arrays);
+  if (hipEventCreate(&d->ev_main[0]) != hipSuccess || hipEventCreate(&d->ev_main[1]) != hipSuccess)
+    d->ev_main[0] = d->ev_main[1] = nullptr;
   if (book1_eligible(s) && book1_upload(d, s) != 0) {
     rt_scene_release(d);
     return NULL;
@@ -615,31 +679,32 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   (void)hipSetDevice(d->device);
   (void)hipFree(d->arena);
   if (d->b1_arena) (void)hipFree(d->b1_arena);
+  for (hipEvent_t e : d->ev_main)
+    if (e) (void)hipEventDestroy(e);
   delete d;
 }
 
-extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out,
-                                    void *stream) {
-  if (!d || !d_out) return rt_set_error("rt_render_rows_async: NULL argument"), -1;
-  if (n_rows <= 0) return 0;
-  if (row0 < 0 || row_stride <= 0 || (int64_t)row0 + (int64_t)(n_rows - 1) * row_stride >= d->height)
-    return rt_set_error("rows %d + k*%d (k < %d) outside image height %d", row0, row_stride, n_rows, d->height), -1;
-  HIP_OK(hipSetDevice(d->device));
-  const int64_t npix = (int64_t)n_rows * d->width;
-  const dim3 grid((unsigned)((npix + kBlock - 1) / kBlock)), block(kBlock);
-  hipStream_t st = (hipStream_t)stream;
-  if (d->book1) {
-    if (npix >= (int64_t)1 << 31) return rt_set_error("too many pixels for one launch"), -1;
-    b1::Book1View V = d->b1view;
-    V.row0 = row0;
-    V.row_stride = row_stride;
-    V.n_rows = n_rows;
-    HIP_OK(hipMemsetAsync(V.work_counter, 0, d->book1_stats ? 256 : sizeof(int32_t), st));
-    if (d->book1_stats) {
-      HIP_OK(hipMemsetAsync(V.stats + 18, 0xff, sizeof(unsigned long long), st));
-      HIP_OK(hipMemsetAsync(V.stats + 21, 0xff, sizeof(unsigned long long), st));
-    }
+// One Book-1 launch of the scene's variant (work counter and stats reset first).
+static int launch_book1(rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st,
+                        bool cost_pass = false) {
+  HIP_OK(hipMemsetAsync(V.work_counter, 0, d->book1_stats ? 256 : sizeof(int32_t), st));
+  if (d->book1_stats) {
+    HIP_OK(hipMemsetAsync(V.stats + 18, 0xff, sizeof(unsigned long long), st));
+    HIP_OK(hipMemsetAsync(V.stats + 21, 0xff, sizeof(unsigned long long), st));
+  }
     const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
+  if (cost_pass) {  // the variants that have an ordered refill (render_batched)
+    if (d->book1_ver == 9 && d->book1_lds)
+      hipLaunchKernelGGL((rt_book1_cost_kernel<true, 9>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    else if (d->book1_ver == 9)
+      hipLaunchKernelGGL((rt_book1_cost_kernel<false, 9>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    else if (d->book1_lds)
+      hipLaunchKernelGGL((rt_book1_cost_kernel<true, 5>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    else
+      hipLaunchKernelGGL((rt_book1_cost_kernel<false, 5>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+    HIP_OK(hipGetLastError());
+    return 0;
+  }
 #define RT_B1_LAUNCH(LDS, VER, ST, ...) \
   hipLaunchKernelGGL((rt_book1_kernel<LDS, VER, ST, ##__VA_ARGS__>), g1, blk, d->b1_lds_bytes, st, V, d_out)
     switch (d->book1_occ * 100 + d->book1_ver * 4 + (d->book1_lds ? 1 : 0) + (d->book1_stats ? 2 : 0)) {
@@ -666,7 +731,43 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       default: return rt_set_error("book1 variant %d not built", d->book1_ver), -1;
     }
 #undef RT_B1_LAUNCH
-    HIP_OK(hipGetLastError());
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out,
+                                    void *stream) {
+  if (!d || !d_out) return rt_set_error("rt_render_rows_async: NULL argument"), -1;
+  if (n_rows <= 0) return 0;
+  if (row0 < 0 || row_stride <= 0 || (int64_t)row0 + (int64_t)(n_rows - 1) * row_stride >= d->height)
+    return rt_set_error("rows %d + k*%d (k < %d) outside image height %d", row0, row_stride, n_rows, d->height), -1;
+  HIP_OK(hipSetDevice(d->device));
+  const int64_t npix = (int64_t)n_rows * d->width;
+  const dim3 grid((unsigned)((npix + kBlock - 1) / kBlock)), block(kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->book1) {
+    if (npix >= (int64_t)1 << 31) return rt_set_error("too many pixels for one launch"), -1;
+    b1::Book1View V = d->b1view;
+    V.row0 = row0;
+    V.row_stride = row_stride;
+    V.n_rows = n_rows;
+    // longest-first order: a low-spp pass measures each work item's traversal steps
+    if (d->lpt && V.S.cam.spp >= 4 * d->lpt_spp && npix >= 4096) {
+      b1::Book1View P = V;
+      P.S.cam.spp = d->lpt_spp;
+      P.cost_out = d->lpt_cost;
+      if (launch_book1(d, P, d_out, st, true) != 0) return -1;
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 512 * sizeof(uint32_t), st));
+      const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+      hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist);
+      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist);
+      hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
+      HIP_OK(hipGetLastError());
+      V.order = d->lpt_order;
+    }
+    if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+    if (launch_book1(d, V, d_out, st) != 0) return -1;
+    if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
     return 0;
   }
   if ((d->features & ~kFeatBook1) == 0)
@@ -814,4 +915,13 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
     snprintf(buf, sizeof buf, "rt_book1_kernel<%s, %d, %s, %d>", d->book1_lds ? "true" : "false", d->book1_ver,
              d->book1_stats ? "true" : "false", d->book1_occ);
   return buf;
+}
+
+// Milliseconds of the last frame launch of rt_render_rows_async on this scene (after it completed);
+// excludes the LPT cost pre-pass.  -1 when unavailable.
+extern "C" double rt_scene_last_launch_ms(rt_device_scene *d) {
+  if (!d || !d->ev_main[0] || !d->ev_main[1]) return -1.0;
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, d->ev_main[0], d->ev_main[1]) != hipSuccess) return -1.0;
+  return (double)ms;
 }

@@ -118,6 +118,8 @@ def lib() -> ctypes.CDLL:
         L.rt_diag_libm.restype = c_int
         L.rt_diag_arith.argtypes = [c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_int]
         L.rt_diag_arith.restype = c_int
+        L.rt_scene_last_launch_ms.argtypes = [c_void_p]
+        L.rt_scene_last_launch_ms.restype = c_double
         L.rt_scene_kernel.argtypes = [c_void_p]
         L.rt_scene_kernel.restype = c_char_p
         L.rt_last_error.restype = c_char_p
@@ -219,6 +221,10 @@ class DeviceScene:
                                         c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
         if rc != 0:
             raise RtcError(f"rt_render_rows_async failed: {last_error()}")
+
+    def last_launch_ms(self) -> float:
+        """Duration of the last frame launch (excludes the cost pre-pass); call after it completed."""
+        return float(lib().rt_scene_last_launch_ms(self._h))
 
     @property
     def kernel_name(self) -> str:
