@@ -69,8 +69,7 @@ int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int de
  * root-leaf steps, idle-in-shade iterations, shader clocks in traversal / shading iterations,
  * wave-level traversal / shading iterations, v6 wave-level box / sphere phases or v5 fast / fallback sphere tests, v5 wave-level sphere-code
  * and fallback executions, clock64 / wall_clock64 ticks of the waves' lifetimes, earliest start / latest end,
- * latest start, first pixel-counter exhaustion (wall_clock64), v5 box hits, cooperative traces and their clocks, v9 cooperative windows and scan steps;
- * n <= 27). */
+ * latest start, first pixel-counter exhaustion (wall_clock64), v5 box hits, cooperative traces and their clocks, v9 cooperative windows and scan steps, and their window / walk clocks; n <= 29). */
 int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out, int n);
 /* Diagnostics (same stats build): per work item of the last launch, {traversal steps, duration in
  * wall_clock64 ticks (100 MHz)} as 2 x uint32 each, for the first n_items items. */

@@ -51,6 +51,10 @@ struct Book1View {
   int32_t reverse;           // hand out work items last-first
   const int32_t *order;      // work item order (longest-first from the cost pre-pass), or null
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
+  const uint32_t *n_coop;    // v9: the first *n_coop items of `order` are rendered by whole waves
+  int32_t *coop_counter;     //     (render_pixel_coop), claimed through this counter
+  int32_t coop_waves;        //     by the first coop_waves waves of the grid
+  const uint32_t *n_heavy;   // the first *n_heavy items of `order`: waves holding one run at priority 3
   int32_t coop_lanes;        // v5: cooperative traversal once the counter is dry and <= this many lanes live
   int32_t experiment;        // stats builds only: timing experiments that change the image (RT_EXPERIMENT)
   unsigned long long *stats; // diagnostic counters (kStats builds only)
@@ -725,7 +729,8 @@ RT_D bool trav_step_v9(const Book1View &V, const float4 *items, Lane &L, float t
   uint32_t next = p + 1;
   if (w & kLeaf9) {
     if (kStats) st[6]++;
-    sphere_test_data<kStats>(q0, (int)(w & 0x7fffffffu), L, tmin, st);
+    if (!(kStats && (V.experiment & 1)))  // timing experiment (stats builds): no sphere tests
+      sphere_test_data<kStats>(q0, (int)(w & 0x7fffffffu), L, tmin, st);
   } else {
     if (kStats) st[5]++;
     const bool hit = aabb_packed(q0, q1, L, tmin);
@@ -919,10 +924,12 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const Lane &L, in
   float tmax = __builtin_inff();
   int hit = -1;
   int p = 0;
-  while (p < n) {
+  int guard = 0;  // every scan step advances p, so n steps bound the walk; this only catches bugs
+  while (p < n && guard <= n) {
     const int base = p;
     const int q = base + lane;
     if (kStats && lane == 0) st[25]++;
+    const long long c_w0 = kStats ? (long long)clock64() : 0;
     float v0 = 0.0f, v1 = 0.0f;  // node: E, X; leaf: root
     uint32_t meta = 0;           // node: skip; leaf: index | kLeaf9
     if (q < n) {
@@ -943,26 +950,115 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const Lane &L, in
       }
     }
     const int end = min(n, base + 64);
-    while (p < end) {
-      if (kStats && lane == 0) st[26]++;
-      const int l = p - base;
-      const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, l);
-      const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0), l));
-      if (m & kLeaf9) {
-        if (!(a <= tmin || a >= tmax)) tmax = a, hit = (int)(m & 0x7fffffffu);
-        p++;
-      } else {
-        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v1), l));
-        p += !(fminf(tmax, x) <= a) ? 1 : (int)m;
-      }
+    long long c_w1 = 0;
+    if (kStats) {
+      __builtin_amdgcn_s_waitcnt(0);
+      c_w1 = (long long)clock64();
+      if (lane == 0) st[27] += c_w1 - c_w0;
     }
+    // decisions for the current t_max in every lane, then a scalar walk along the next-pointers;
+    // an accepted sphere changes t_max, so the decisions are redone from there
+    const bool leaf = (meta & kLeaf9) != 0;
+    const int l = lane;
+    while (p < end && guard++ <= n) {
+      const bool take = leaf ? !(v0 <= tmin || v0 >= tmax) : !(fminf(tmax, v1) <= v0);
+      // next item after this one for the current t_max; an accepted sphere (t_max changes) is
+      // encoded as kStop + its position so that the walk below only has to test one bound
+      constexpr int kStop = 1 << 20;
+      const int next = leaf ? (take ? kStop + l : l + 1) : (take ? l + 1 : l + (int)meta);
+      const int wend = end - base;
+      int at = p - base;
+      while (at < wend) at = __builtin_amdgcn_readlane(next, at);
+      if (at < kStop) {  // left the window
+        p = base + at;
+        break;
+      }
+      at -= kStop;  // an accepted sphere: t_max shrinks, the walk goes on after it
+      tmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0), at));
+      hit = (int)((uint32_t)__builtin_amdgcn_readlane((int)meta, at) & 0x7fffffffu);
+      p = base + at + 1;
+    }
+    if (kStats && lane == 0) st[28] += (long long)clock64() - c_w1;
   }
   out_tmax = tmax;
   out_hit = hit;
 }
 
+// A whole pixel (all its samples, in order) rendered by one wave: the path state is wave-uniform
+// (every lane holds the same values and runs the same shading), and each ray is traced with
+// coop_trace9.  For the few pixels whose sequential chain is far longer than the frame's fair share
+// (the LPT pre-pass finds them), this trades 64 lanes of throughput for a much shorter chain.
+RT_D void render_pixel_coop(const Book1View &V, const float4 *items9, int64_t pix, uint8_t *__restrict__ out,
+                            int glane) {
+  const rt_camera &cam = V.S.cam;
+  const int W = cam.width;
+  const int jj = (int)(pix / W);
+  const int i = (int)(pix - (int64_t)jj * W);
+  const int j = V.row0 + jj * V.row_stride;
+  const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
+  const float tmin = 1e-3f;
+  Pcg32 g;
+  g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
+  f3 acc = mk(0.0f, 0.0f, 0.0f);
+  Lane L;
+  L.ix = L.iy = L.iz = 0.0f;
+  L.hit = -1;
+  L.cur = 0;
+  L.pend0 = L.pend1 = 0xffffu;
+  L.sp = L.k = 0;
+  for (int s = 0; s < cam.spp; s++) {
+    // camera ray (src/raytracing.c:96-122)
+    const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+    const float px = g.between(-0.5f, 0.5f);
+    const float py = g.between(-0.5f, 0.5f);
+    f3 o = lf;
+    if (cam.dof_angle > 0.0f) {
+      float a, b;
+      for (;;) {
+        a = g.between(-1.0f, 1.0f);
+        b = g.between(-1.0f, 1.0f);
+        if (a * a + b * b < 1.0f) break;
+      }
+      o = add(add(lf, scale(ld3(cam.disc_u), a)), scale(ld3(cam.disc_v), b));
+    }
+    f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+    Record R;
+    R.r0 = R.r1 = 0;
+    R.n = 0;
+    f3 tail = mk(0.0f, 0.0f, 0.0f);
+    for (int depth = cam.max_depth; depth > 0;) {  // Camera_ray_color (src/raytracing.c:39-75)
+      L.ox = o.x, L.oy = o.y, L.oz = o.z;
+      L.dx = d.x, L.dy = d.y, L.dz = d.z;
+      L.ix = 1.0f / d.x, L.iy = 1.0f / d.y, L.iz = 1.0f / d.z;
+      L.a = dot(d, d);
+      L.fast = L.a >= kDivLo && L.a <= kDivHi;
+      L.ra = recip_core(L.a);
+      float tmax;
+      int hit;
+      coop_trace9(V, items9, L, 0, tmin, tmax, hit);
+      if (hit < 0) {
+        tail = ld3(cam.background);
+        break;
+      }
+      const rt_sphere &sp = V.S.spheres[hit];
+      const f3 p = ray_at(o, d, tmax);
+      const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
+      const bool front = dot(d, outward) < 0.0f;
+      const f3 normal = front ? outward : neg(outward);
+      const FastMat &m = V.mats[sp.material];
+      const f3 nd = scatter(m, normal, front, d, g);
+      rec_push(V, R, (uint32_t)sp.material, glane);
+      o = p;
+      d = nd;
+      depth--;
+    }
+    acc = add(acc, rec_fold(V, R, tail, glane));
+  }
+  if (__lane_id() == 0) write_pixel(out + pix * 3, acc, cam.spp);
+}
+
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
-constexpr int kNumStats = 27;
+constexpr int kNumStats = 29;
 constexpr int kSteps = 4;
 
 // kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
@@ -1017,7 +1113,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   //        wave start / latest wave end, 20 latest wave start, 21 first time the pixel counter ran
   //        dry (wall_clock64; the host presets 18 and 21 to ~0), 22 (v5) box tests that hit,
   //        23 cooperative traces, 24 clocks in cooperative traces (lane 0), 25/26 (v9) cooperative
-  //        windows / scan steps
+  //        windows / scan steps, 27/28 (v9) clocks in cooperative window evaluation / walks
   unsigned long long st[kNumStats] = {};
   long long t_iter = kStats ? (long long)clock64() : 0;
   const long long t_start = t_iter, w_start = kStats ? (long long)wall_clock64() : 0;
@@ -1042,6 +1138,28 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   L.pend0 = L.pend1 = 0xffffu;
   L.sp = L.k = 0;
 
+  // the heaviest pixels first, one per wave (render_pixel_coop), on the grid's first coop_waves waves
+  int64_t work_offset = 0;  // the lanes' own items start after the cooperative ones
+  if (kStep == 9 && kLds && V.n_coop != nullptr) {
+    const int64_t n_coop = (int64_t)*V.n_coop;
+    work_offset = n_coop;
+    if (glane / 64 < V.coop_waves) {
+      for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(V.coop_counter, 1);
+        k = __shfl(k, 0);
+        if (k >= n_coop) break;
+        __builtin_amdgcn_s_setprio(3);  // these chains set the frame time: issue before the lane-parallel waves
+        render_pixel_coop(V, items9, (int64_t)V.order[k], out, glane);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  const int64_t total_own = total - work_offset;
+  const int64_t n_heavy = (V.order && V.n_heavy) ? (int64_t)*V.n_heavy : 0;
+  bool heavy = false;  // this lane's pixel is among the n_heavy longest
+  bool prio = false;
+
   for (;;) {
     const uint64_t trav = __ballot(mode == kTrav);
     const uint64_t wait = __ballot(mode == kWait);
@@ -1051,6 +1169,16 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       t_iter = now;
     }
     if ((trav | wait) == 0) break;
+    if (n_heavy > 0) {  // the longest pixels' waves issue first: their chains set the frame time
+      const bool want_prio = __ballot(heavy && mode != kExit) != 0;
+      if (want_prio != prio) {
+        prio = want_prio;
+        if (prio)
+          __builtin_amdgcn_s_setprio(3);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
+    }
     // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
@@ -1169,12 +1297,13 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
         base = __shfl(base, first);
         pix = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
-        if (pix >= total) {
+        if (pix >= total_own) {
           if (kStats && mode != kExit) atomicMin(&V.stats[21], (unsigned long long)wall_clock64());
           mode = kExit;
           break;
         }
-        if (V.order) pix = V.order[pix];  // longest work items first
+        heavy = pix + work_offset < n_heavy;
+        if (V.order) pix = V.order[pix + work_offset];  // longest work items first
         else if (V.reverse) pix = total - 1 - pix;
         const int jj = (int)(pix / W);
         i = (int)(pix - (int64_t)jj * W);
@@ -1244,6 +1373,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     atomicAdd(&V.stats[24], st[24]);
     atomicAdd(&V.stats[25], st[25]);
     atomicAdd(&V.stats[26], st[26]);
+    atomicAdd(&V.stats[27], st[27]);
+    atomicAdd(&V.stats[28], st[28]);
     if (lane == 0) {  // 18/19: earliest wave start, latest wave end (wall_clock64 ticks)
       atomicMin(&V.stats[18], (unsigned long long)w_start);
       atomicMax(&V.stats[19], (unsigned long long)wall_clock64());

@@ -175,6 +175,13 @@ __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c) {
   const uint32_t k = (uint32_t)e * 8u + frac;
   return k > 255u ? 255u : k;
 }
+static uint32_t host_lpt_bucket(uint32_t c) {  // lpt_bucket on the host
+  c |= 1u;
+  const int e = 31 - __builtin_clz(c);
+  const uint32_t frac = e >= 3 ? (c >> (e - 3)) & 7u : (c << (3 - e)) & 7u;
+  const uint32_t k = (uint32_t)e * 8u + frac;
+  return k > 255u ? 255u : k;
+}
 __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist) {
   __shared__ uint32_t h[256];
   for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
@@ -185,13 +192,21 @@ __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist) {
   for (int k = threadIdx.x; k < 256; k += blockDim.x)
     if (h[k]) atomicAdd(&hist[k], h[k]);
 }
-__global__ void lpt_scan_kernel(uint32_t *hist) {  // one thread: offsets, highest bucket first
+// one thread: offsets, highest bucket first; hist[512] = items in buckets above `coop_bucket`
+// (rendered by whole waves, render_pixel_coop), hist[513] = their claim counter
+// hist[514] = items in buckets above `prio_bucket` (their waves run at raised priority)
+__global__ void lpt_scan_kernel(uint32_t *hist, int coop_bucket, int prio_bucket) {
   if (threadIdx.x != 0) return;
-  uint32_t run = 0;
+  uint32_t run = 0, coop = 0, heavy = 0;
   for (int k = 255; k >= 0; k--) {
     hist[256 + k] = run;
     run += hist[k];
+    if (k > coop_bucket) coop += hist[k];
+    if (k > prio_bucket) heavy += hist[k];
   }
+  hist[512] = coop;
+  hist[513] = 0;
+  hist[514] = heavy;
 }
 __global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -219,7 +234,10 @@ struct rt_device_scene {
   int lpt_spp = 8;
   uint32_t *lpt_cost = nullptr;  // steps per work item (W*H)
   int32_t *lpt_order = nullptr;  // work item order (W*H)
-  uint32_t *lpt_hist = nullptr;  // 256 bucket counts + 256 running offsets
+  uint32_t *lpt_hist = nullptr;  // 256 bucket counts, 256 running offsets, cooperative count + counter
+  int coop_steps = 650;          // pre-pass traversal steps per sample above which a pixel goes to a whole wave
+  int coop_waves = 512;          // waves that render those pixels first (0: off)
+  int prio_steps = 0;            // pre-pass steps per sample above which a pixel's wave runs at priority 3
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
   int b1_grid = 0;
   size_t b1_lds_bytes = 0;
@@ -533,7 +551,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
-                           512 * sizeof(uint32_t)};                                          // [12] LPT buckets
+                           1024 * sizeof(uint32_t)};                                         // [12] LPT buckets
   for (int k = 0; k < 13; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
@@ -574,6 +592,18 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   }
   V.order = nullptr;
   V.cost_out = nullptr;
+  V.n_coop = nullptr;
+  V.coop_counter = nullptr;
+  V.coop_waves = 0;
+  {
+    const char *e1 = getenv("RT_COOP_STEPS"), *e2 = getenv("RT_COOP_WAVES");
+    d->coop_steps = (e1 && *e1) ? atoi(e1) : 650;
+    d->coop_waves = (e2 && *e2) ? atoi(e2) : 512;
+    if (d->book1_ver != 9 || !d->book1_lds) d->coop_waves = 0;
+    const char *e3 = getenv("RT_PRIO_STEPS");
+    d->prio_steps = (e3 && *e3) ? atoi(e3) : 0;  // off by default: measured no gain
+  }
+  V.n_heavy = nullptr;
   V.n_items9 = (int32_t)(items9.size() / 2) - 1;  // without the trailing pad item
   V.n_items9_alloc = (int32_t)(items9.size() / 2);
   V.spill_lanes = spill_lanes;
@@ -586,7 +616,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     V.shade_batch = (eb && *eb) ? atoi(eb) : 48;
     V.shade_batch = V.shade_batch < 1 ? 1 : (V.shade_batch > 64 ? 64 : V.shade_batch);  // >= 1: progress
     const char *ex = getenv("RT_EXPERIMENT");
-    V.experiment = (ex && *ex && d->book1_stats) ? atoi(ex) : 0;
+    V.experiment = (ex && *ex) ? atoi(ex) : 0;  // bit 0 (stats builds): no sphere tests; bit 1: coop printf
     const char *ec = getenv("RT_COOP_LANES");
     V.coop_lanes = (ec && *ec) ? atoi(ec) : 0;  // off: measured slower than the DFS lanes
     if ((d->book1_ver == 5 && (s->n_bvh > 64 * b1::kCoopSlots || s->n_spheres > 64 * b1::kCoopSlots)) ||
@@ -757,13 +787,32 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       P.S.cam.spp = d->lpt_spp;
       P.cost_out = d->lpt_cost;
       if (launch_book1(d, P, d_out, st, true) != 0) return -1;
-      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 512 * sizeof(uint32_t), st));
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 1024 * sizeof(uint32_t), st));
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist);
-      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist);
+      const int64_t thr = (int64_t)d->coop_steps * d->lpt_spp;
+      const int coop_bucket = d->coop_waves > 0 && thr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)thr) : 256;
+      const int64_t pthr = (int64_t)d->prio_steps * d->lpt_spp;
+      const int prio_bucket = d->prio_steps > 0 && pthr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)pthr) : 256;
+      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, coop_bucket, prio_bucket);
       hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
       HIP_OK(hipGetLastError());
       V.order = d->lpt_order;
+      V.n_heavy = d->prio_steps > 0 ? d->lpt_hist + 514 : nullptr;
+      if (env_flag("RT_DEBUG", false)) {  // diagnostic: synchronous peek at the cooperative count
+        uint32_t nc = 0;
+        HIP_OK(hipStreamSynchronize(st));
+        HIP_OK(hipMemcpy(&nc, d->lpt_hist + 512, sizeof nc, hipMemcpyDeviceToHost));
+        uint32_t nh = 0;
+        HIP_OK(hipMemcpy(&nh, d->lpt_hist + 514, sizeof nh, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[rtc] lpt: %lld items, %u cooperative (threshold %d steps/sample, %d waves), %u at raised "
+                "priority (threshold %d)\n", (long long)npix, nc, d->coop_steps, d->coop_waves, nh, d->prio_steps);
+      }
+      if (d->coop_waves > 0) {
+        V.n_coop = d->lpt_hist + 512;
+        V.coop_counter = (int32_t *)(d->lpt_hist + 513);
+        V.coop_waves = d->coop_waves;
+      }
     }
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
     if (launch_book1(d, V, d_out, st) != 0) return -1;

@@ -11,7 +11,7 @@ import rtc  # noqa: E402
 
 L = rtc.lib()
 L.rt_book1_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-N = 27
+N = 29
 for batch in os.environ.get("BATCHES", "48").split(","):
     os.environ["RT_SHADE_BATCH"] = batch.split(":")[0]
     if ":" in batch:
@@ -41,7 +41,7 @@ for batch in os.environ.get("BATCHES", "48").split(","):
           f"kernel_ms={kernel_ms:.1f} clock64_per_wave={st[16]/n_waves:.3e} => clock64 MHz~{st[16]/n_waves/kernel_ms/1e3:.0f} "
           f"wall_ticks_per_wave={st[17]/n_waves:.3e} span_wall_ticks={st[19]-st[18]:.4e} => wall MHz~{(st[19]-st[18])/kernel_ms/1e3:.1f} "
           f"concurrency~{st[17]/max(st[19]-st[18],1):.0f} waves last_start_at={(st[20]-st[18])/(st[19]-st[18]):.3f} "
-          f"counter_dry_at={(st[21]-st[18])/(st[19]-st[18]):.3f} (fractions of the span) box_hits/ray={st[22]/st[4]:.2f} coop_traces={st[23]:.3e} windows/coop={st[25]/max(st[23],1):.1f} scan/coop={st[26]/max(st[23],1):.1f}", flush=True)
+          f"counter_dry_at={(st[21]-st[18])/(st[19]-st[18]):.3f} (fractions of the span) box_hits/ray={st[22]/st[4]:.2f} coop_traces={st[23]:.3e} windows/coop={st[25]/max(st[23],1):.1f} scan/coop={st[26]/max(st[23],1):.1f} clk/window={st[27]/max(st[25],1):.0f} walk_clk/window={st[28]/max(st[25],1):.0f}", flush=True)
     if os.environ.get("PIXEL_COST"):
         import numpy as np
         L.rt_book1_pixel_cost.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
