@@ -53,7 +53,7 @@ struct Book1View {
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   const uint32_t *n_coop;    // v9: the first *n_coop items of `order` are rendered by whole waves
   int32_t *coop_counter;     //     (render_pixel_coop), claimed through this counter
-  int32_t coop_waves;        //     by the first coop_waves waves of the grid
+  const uint32_t *coop_waves_dev;  // by the first *coop_waves_dev waves of the grid
   const uint32_t *n_heavy;   // the first *n_heavy items of `order`: waves holding one run at priority 3
   int32_t coop_lanes;        // v5: cooperative traversal once the counter is dry and <= this many lanes live
   int32_t experiment;        // stats builds only: timing experiments that change the image (RT_EXPERIMENT)
@@ -1143,7 +1143,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   if (kStep == 9 && kLds && V.n_coop != nullptr) {
     const int64_t n_coop = (int64_t)*V.n_coop;
     work_offset = n_coop;
-    if (glane / 64 < V.coop_waves) {
+    if (glane / 64 < (int)*V.coop_waves_dev) {
       for (;;) {
         int k = 0;
         if (lane == 0) k = atomicAdd(V.coop_counter, 1);

@@ -182,32 +182,80 @@ static uint32_t host_lpt_bucket(uint32_t c) {  // lpt_bucket on the host
   const uint32_t k = (uint32_t)e * 8u + frac;
   return k > 255u ? 255u : k;
 }
-__global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist) {
+__global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist, unsigned long long *sums) {
   __shared__ uint32_t h[256];
-  for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
+  __shared__ unsigned long long w[256];
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0, w[k] = 0;
   __syncthreads();
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicAdd(&h[lpt_bucket(cost[i])], 1u);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t b = lpt_bucket(cost[i]);
+    atomicAdd(&h[b], 1u);
+    atomicAdd(&w[b], (unsigned long long)cost[i]);
+  }
   __syncthreads();
-  for (int k = threadIdx.x; k < 256; k += blockDim.x)
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) {
     if (h[k]) atomicAdd(&hist[k], h[k]);
+    if (w[k]) atomicAdd(&sums[k], w[k]);
+  }
 }
-// one thread: offsets, highest bucket first; hist[512] = items in buckets above `coop_bucket`
-// (rendered by whole waves, render_pixel_coop), hist[513] = their claim counter
-// hist[514] = items in buckets above `prio_bucket` (their waves run at raised priority)
-__global__ void lpt_scan_kernel(uint32_t *hist, int coop_bucket, int prio_bucket) {
+
+// Cost model of one launch for the split between whole-wave pixels (render_pixel_coop) and lane
+// pixels, in clocks (measured on the headline frame): a lane pixel advances one
+// traversal step per kDfsStep clocks, the lanes together at kDfsUse of that rate; a whole-wave
+// pixel costs kCoopStep clocks per step.  The frame ends when both the slowest lane pixel and the
+// whole-wave queue are done.
+struct LptModel {
+  float spp_ratio;  // frame spp / pre-pass spp (costs are pre-pass steps)
+  int grid_waves;
+};
+constexpr float kDfsStep = 1700.0f, kDfsUse = 0.7f, kCoopStep = 400.0f;
+
+// one thread: offsets, highest bucket first; hist[512] = items in buckets above the chosen split
+// (rendered by whole waves), hist[513] = their claim counter, hist[514] = items above `prio_bucket`
+// (raised priority), hist[515] = whole waves.  coop_bucket / coop_waves < 0: chosen by the model.
+__global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, int coop_bucket, int coop_waves,
+                                int prio_bucket, LptModel m) {
   if (threadIdx.x != 0) return;
-  uint32_t run = 0, coop = 0, heavy = 0;
+  uint32_t run = 0, heavy = 0;
   for (int k = 255; k >= 0; k--) {
     hist[256 + k] = run;
     run += hist[k];
-    if (k > coop_bucket) coop += hist[k];
     if (k > prio_bucket) heavy += hist[k];
   }
-  hist[512] = coop;
+  double total = 0.0;
+  for (int k = 0; k < 256; k++) total += (double)sums[k];
+  int best_b = coop_bucket >= 0 ? coop_bucket : 255, best_w = coop_waves >= 0 ? coop_waves : 0;
+  if (coop_bucket < 0 || coop_waves < 0) {
+    // highest non-empty bucket at or below each bucket (the largest lane pixel of a split)
+    int16_t top_of[256];
+    for (int k = 0, t = -1; k < 256; k++) top_of[k] = (int16_t)(t = hist[k] ? k : t);
+    double best_t = 1e300;
+    for (int wc = 0; wc <= m.grid_waves / 2; wc = wc ? 2 * wc : 128) {
+      if (coop_waves >= 0 && wc != coop_waves) continue;
+      double coop_work = 0.0;  // steps above the split
+      for (int b = 255; b >= -1; b--) {
+        if (b < 255) coop_work += (double)sums[b + 1];
+        if (coop_bucket >= 0 && b != coop_bucket) continue;
+        if (wc == 0 && coop_work > 0.0) break;
+        // the largest lane pixel: the top of bucket b (or of the highest non-empty one)
+        const int top = b < 0 ? -1 : top_of[b];
+        const double maxc = top < 0 ? 0.0 : ldexp((double)(9 + (top & 7)) / 8.0, top >> 3) * m.spp_ratio;
+        const double lanes = (double)(m.grid_waves - wc) * 64.0;
+        const double t_dfs = fmax(maxc * kDfsStep, (total - coop_work) * m.spp_ratio * kDfsStep / (lanes * kDfsUse));
+        const double t_coop = wc ? coop_work * m.spp_ratio * kCoopStep / wc : 0.0;
+        const double t = fmax(t_dfs, t_coop);
+        if (t < best_t) best_t = t, best_b = b, best_w = wc;
+      }
+    }
+  }
+  uint32_t coop = 0;
+  for (int k = 255; k > best_b; k--) coop += hist[k];
+  hist[512] = best_w > 0 ? coop : 0;
   hist[513] = 0;
   hist[514] = heavy;
+  hist[515] = (uint32_t)best_w;
 }
+
 __global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
@@ -235,8 +283,8 @@ struct rt_device_scene {
   uint32_t *lpt_cost = nullptr;  // steps per work item (W*H)
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // 256 bucket counts, 256 running offsets, cooperative count + counter
-  int coop_steps = 650;          // pre-pass traversal steps per sample above which a pixel goes to a whole wave
-  int coop_waves = 512;          // waves that render those pixels first (0: off)
+  int coop_steps = -1;           // pre-pass steps per sample above which a pixel goes to a whole wave (-1: model)
+  int coop_waves = -1;           // waves that render those pixels first (0: off, -1: model)
   int prio_steps = 0;            // pre-pass steps per sample above which a pixel's wave runs at priority 3
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
   int b1_grid = 0;
@@ -551,7 +599,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
-                           1024 * sizeof(uint32_t)};                                         // [12] LPT buckets
+                           4096};                                                            // [12] LPT buckets
   for (int k = 0; k < 13; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
@@ -594,11 +642,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.cost_out = nullptr;
   V.n_coop = nullptr;
   V.coop_counter = nullptr;
-  V.coop_waves = 0;
+  V.coop_waves_dev = nullptr;
   {
     const char *e1 = getenv("RT_COOP_STEPS"), *e2 = getenv("RT_COOP_WAVES");
-    d->coop_steps = (e1 && *e1) ? atoi(e1) : 650;
-    d->coop_waves = (e2 && *e2) ? atoi(e2) : 512;
+    d->coop_steps = (e1 && *e1) ? atoi(e1) : -1;  // -1: split chosen by the cost model (lpt_scan_kernel)
+    d->coop_waves = (e2 && *e2) ? atoi(e2) : -1;
     if (d->book1_ver != 9 || !d->book1_lds) d->coop_waves = 0;
     const char *e3 = getenv("RT_PRIO_STEPS");
     d->prio_steps = (e3 && *e3) ? atoi(e3) : 0;  // off by default: measured no gain
@@ -787,14 +835,19 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       P.S.cam.spp = d->lpt_spp;
       P.cost_out = d->lpt_cost;
       if (launch_book1(d, P, d_out, st, true) != 0) return -1;
-      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 1024 * sizeof(uint32_t), st));
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 4096, st));
+      unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);  // after the 516 counters
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
-      hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist);
+      hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
       const int64_t thr = (int64_t)d->coop_steps * d->lpt_spp;
-      const int coop_bucket = d->coop_waves > 0 && thr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)thr) : 256;
+      const int coop_bucket = d->coop_steps < 0 ? -1 : (thr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)thr) : 255);
+      LptModel model;
+      model.spp_ratio = (float)V.S.cam.spp / (float)d->lpt_spp;
+      model.grid_waves = d->b1_grid * (b1::kBlock / 64);
       const int64_t pthr = (int64_t)d->prio_steps * d->lpt_spp;
       const int prio_bucket = d->prio_steps > 0 && pthr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)pthr) : 256;
-      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, coop_bucket, prio_bucket);
+      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, coop_bucket,
+                         d->coop_waves, prio_bucket, model);
       hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
       HIP_OK(hipGetLastError());
       V.order = d->lpt_order;
@@ -803,15 +856,16 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
         uint32_t nc = 0;
         HIP_OK(hipStreamSynchronize(st));
         HIP_OK(hipMemcpy(&nc, d->lpt_hist + 512, sizeof nc, hipMemcpyDeviceToHost));
-        uint32_t nh = 0;
+        uint32_t nh = 0, nw = 0;
         HIP_OK(hipMemcpy(&nh, d->lpt_hist + 514, sizeof nh, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[rtc] lpt: %lld items, %u cooperative (threshold %d steps/sample, %d waves), %u at raised "
-                "priority (threshold %d)\n", (long long)npix, nc, d->coop_steps, d->coop_waves, nh, d->prio_steps);
+        HIP_OK(hipMemcpy(&nw, d->lpt_hist + 515, sizeof nw, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[rtc] lpt: %lld items, %u cooperative on %u waves (RT_COOP_STEPS %d, RT_COOP_WAVES %d; <0: "
+                "model), %u at raised priority\n", (long long)npix, nc, nw, d->coop_steps, d->coop_waves, nh);
       }
-      if (d->coop_waves > 0) {
+      if (d->coop_waves != 0) {
         V.n_coop = d->lpt_hist + 512;
         V.coop_counter = (int32_t *)(d->lpt_hist + 513);
-        V.coop_waves = d->coop_waves;
+        V.coop_waves_dev = d->lpt_hist + 515;
       }
     }
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
