@@ -119,6 +119,16 @@ RT_D float diag_float(uint64_t h, int emin, int emax) {  // random sign/mantissa
 }
 __global__ void rt_diag_arith_kernel(int fn, uint64_t start, uint64_t count, uint64_t seed,
                                      unsigned long long *mism) {
+  if (fn == 3) {  // timing: a dependent v_readlane chain, clocks per hop
+    const int lane = __lane_id();
+    const int next = (lane + 1 + (int)(seed & 7)) & 63;
+    int at = 0;
+    const long long t0 = (long long)clock64();
+    for (uint64_t k = 0; k < count; k++) at = __builtin_amdgcn_readlane(next, at);
+    const long long t1 = (long long)clock64();
+    if (lane == 0) mism[0] = (unsigned long long)((t1 - t0) * 1000 / (long long)(count ? count : 1)) + (at == 1000 ? 1 : 0);
+    return;
+  }
   unsigned long long bad = 0;
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (uint64_t)gridDim.x * blockDim.x) {
     if (fn == 0) {
@@ -987,12 +997,13 @@ extern "C" int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_
 
 extern "C" int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches,
                              int device) {
-  if (fn < 0 || fn > 2 || mismatches == NULL) return rt_set_error("rt_diag_arith: bad arguments"), -1;
+  if (fn < 0 || fn > 3 || mismatches == NULL) return rt_set_error("rt_diag_arith: bad arguments"), -1;
   HIP_OK(hipSetDevice(device));
   unsigned long long *dm = NULL;
   HIP_OK(hipMalloc(&dm, sizeof *dm));
   HIP_OK(hipMemset(dm, 0, sizeof *dm));
-  hipLaunchKernelGGL(rt_diag_arith_kernel, dim3(4096), dim3(256), 0, 0, fn, start, count, seed, dm);
+  hipLaunchKernelGGL(rt_diag_arith_kernel, dim3(fn == 3 ? 1 : 4096), dim3(fn == 3 ? 64 : 256), 0, 0, fn, start, count,
+                     seed, dm);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpy(mismatches, dm, sizeof *dm, hipMemcpyDeviceToHost));
   HIP_OK(hipFree(dm));
