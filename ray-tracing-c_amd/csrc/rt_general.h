@@ -1,0 +1,177 @@
+// rt_general.h — persistent, lane-refilling render loop for every scene (Book-2 features: quads,
+// transforms, constant media, light sampling, textures).  Same arithmetic and call order as
+// rt_device.h's render_pixel / path_color (bit-exact with the reference); different execution
+// structure: the per-pixel sample loop and the per-sample bounce loop are flattened into one
+// per-lane state machine, one bounce per iteration, and a lane that finishes its pixel takes the
+// next one (wave ballot + one atomic), optionally in the longest-first order of a cost pre-pass.
+// The one-lane-per-pixel kernel (rt_render_rows_kernel) keeps every lane of a wave waiting for the
+// wave's slowest pixel; here a wave only waits for its slowest ray of the current bounce.
+#pragma once
+#include "rt_device.h"
+
+namespace rt {
+namespace gen {
+
+constexpr int kBlock = 256;
+
+struct GeneralView {
+  DScene S;
+  int32_t row0, row_stride, n_rows;
+  int32_t *work_counter;     // zeroed before each launch
+  const int32_t *order;      // work item order (longest-first), or null
+  uint32_t *cost_out;        // cost pass: rays traced per work item, or null
+};
+
+template <int F>
+__device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) {
+  const DScene &S = V.S;
+  constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
+  const int W = S.cam.width;
+  const int64_t total = (int64_t)V.n_rows * W;
+  const int lane = __lane_id();
+  const f3 du = ld3(S.cam.delta_u), dv = ld3(S.cam.delta_v), lf = ld3(S.cam.origin);
+  const bool dof = S.cam.dof_angle > 0.0f;
+  const float prob = S.cam.light_prob;
+  const int spp = S.cam.spp;
+
+  // per-lane path state (path_color's locals, kept across iterations)
+  f3 rec_a[kMaxDepth];
+  f3 rec_e[kFull ? kMaxDepth : 1];
+  float rec_w[kFull ? kMaxDepth : 1];
+  uint64_t weighted = 0;
+  int n = 0, depth = 0, s = 0, i = 0, j = 0;
+  int64_t pix = 0;
+  uint32_t rays = 0;
+  Pcg32 g;
+  g.state = 0;
+  g.inc = 0;
+  f3 acc = mk(0.0f, 0.0f, 0.0f), o = acc, d = acc, pixel_pos = acc;
+  bool need_pixel = true, need_sample = true, done = false;
+
+  for (;;) {
+    // ---- refill (src/raytracing.c:93-94): lanes without a pixel take the next ones
+    const uint64_t want = __ballot(need_pixel && !done);
+    if (want) {
+      const int first = __builtin_ctzll(want);
+      int base = 0;
+      if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
+      base = __shfl(base, first);
+      if (need_pixel && !done) {
+        const int64_t k = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
+        if (k >= total) {
+          done = true;
+        } else {
+          pix = V.order ? (int64_t)V.order[k] : k;
+          const int jj = (int)(pix / W);
+          i = (int)(pix - (int64_t)jj * W);
+          j = V.row0 + jj * V.row_stride;
+          g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));
+          pixel_pos = add(add(ld3(S.cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
+          acc = mk(0.0f, 0.0f, 0.0f);
+          s = 0;
+          rays = 0;
+          need_pixel = false;
+          need_sample = spp > 0;
+        }
+      }
+    }
+    if (__ballot(!done) == 0) break;
+    if (done) continue;
+    bool write = spp <= 0 && !need_pixel;  // no samples: the mean is 0/0 (src/raytracing.c:127)
+    // ---- camera ray (src/raytracing.c:100-122)
+    if (need_sample && !write) {
+      const float px = g.between(-0.5f, 0.5f);
+      const float py = g.between(-0.5f, 0.5f);
+      o = lf;
+      if (dof) {
+        float a, b;
+        for (;;) {
+          a = g.between(-1.0f, 1.0f);
+          b = g.between(-1.0f, 1.0f);
+          if (a * a + b * b < 1.0f) break;
+        }
+        o = add(add(lf, scale(ld3(S.cam.disc_u), a)), scale(ld3(S.cam.disc_v), b));
+      }
+      d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
+      depth = S.cam.max_depth;
+      n = 0;
+      weighted = 0;
+      need_sample = false;
+    }
+    // ---- one bounce of path_color (rt_device.h; src/raytracing.c:39-75)
+    bool path_done = false;
+    f3 tail = mk(0.0f, 0.0f, 0.0f);
+    if (write) {
+      // straight to the pixel write
+    } else if (depth <= 0) {
+      path_done = true;
+    } else {
+      Hit h;
+      rays++;
+      if (!trace<F>(S, o, d, 1e-3f, g, h)) {
+        tail = ld3(S.cam.background);
+        path_done = true;
+      } else {
+        Rec r;
+        make_record<F>(S, o, d, h, r);
+        const f3 e = emit<F>(S, r);
+        f3 dir, albedo;
+        bool skip_pdf;
+        if (!scatter<F>(S, r, d, g, dir, albedo, skip_pdf)) {
+          tail = e;
+          path_done = true;
+        } else {
+          rec_a[n] = albedo;
+          if (kFull) {
+            rec_e[n] = e;
+            if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
+              if (g.f32() < prob) dir = lights_rand(S, r.p, g);
+              const float sp = scatter_pdf(S, r.material, r.normal, dir);
+              const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, dir);
+              rec_w[n] = sp / spdf;
+              weighted |= 1ull << n;
+            }
+          }
+          n++;
+          o = r.p;
+          d = dir;
+          depth--;
+        }
+      }
+    }
+    if (!path_done && !write) continue;
+    if (!write) {
+    // ---- fold innermost-first, accumulate, next sample / pixel (src/raytracing.c:124-131)
+    f3 c = tail;
+    for (int k = n - 1; k >= 0; k--) {
+      f3 x = mul(rec_a[k], c);
+      if (kFull) {
+        if ((weighted >> k) & 1) x = scale(x, rec_w[k]);
+        c = add(rec_e[k], x);
+      } else {
+        c = add(mk(0.0f, 0.0f, 0.0f), x);
+      }
+    }
+    acc = add(acc, c);
+    s++;
+    if (s < spp) {
+      need_sample = true;
+      continue;
+    }
+    }
+    const float spp_f = (float)spp;
+    const float ch[3] = {acc.x, acc.y, acc.z};
+    uint8_t *dst = out + pix * 3;
+    for (int q = 0; q < 3; q++) {
+      float v = sqrtf(ch[q] / spp_f);
+      v = v > 0.0f ? v : 0.0f;
+      v = v < 0.999f ? v : 0.999f;
+      dst[q] = (uint8_t)(int)(256.0f * v);
+    }
+    if (V.cost_out) V.cost_out[pix] = rays;
+    need_pixel = true;
+  }
+}
+
+}  // namespace gen
+}  // namespace rt

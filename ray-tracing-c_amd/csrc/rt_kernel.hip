@@ -21,6 +21,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_book1.h"
+#include "rt_general.h"
 #include "rt_device.h"
 
 using namespace rt;
@@ -77,6 +78,12 @@ template <bool kLds, int kVer>
 __global__ __launch_bounds__(b1::kBlock) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, false, kVer>(V, out, lds);
+}
+
+// Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
+template <int F>
+__global__ __launch_bounds__(gen::kBlock) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
+  gen::render_general<F>(V, out);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -297,6 +304,11 @@ struct rt_device_scene {
   int coop_waves = -1;           // waves that render those pixels first (0: off, -1: model)
   int prio_steps = 0;            // pre-pass steps per sample above which a pixel's wave runs at priority 3
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
+  // persistent general path (rt_general.h) for scenes outside the Book-1 path
+  bool general = false;
+  void *gen_arena = nullptr;
+  int32_t *gen_counter = nullptr;
+  int gen_grid = 0;
   int b1_grid = 0;
   size_t b1_lds_bytes = 0;
 };
@@ -702,6 +714,44 @@ extern "C" int rt_device_count(void) {
 
 extern "C" void rt_scene_release(rt_device_scene *d);
 
+// Buffers of the persistent general path: work counter, longest-first cost / order / buckets.
+static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
+  const size_t npix = (size_t)s->camera.width * s->camera.height;
+  const size_t sizes[4] = {256, npix * sizeof(uint32_t), npix * sizeof(int32_t), 4096};
+  size_t off[4], total = 0;
+  for (int k = 0; k < 4; k++) {
+    off[k] = total;
+    total = align_up(total + sizes[k], 256);
+  }
+  void *arena = nullptr;
+  HIP_OK(hipMalloc(&arena, total));
+  char *b = (char *)arena;
+  d->gen_arena = arena;
+  d->gen_counter = (int32_t *)(b + off[0]);
+  d->lpt_cost = (uint32_t *)(b + off[1]);
+  d->lpt_order = (int32_t *)(b + off[2]);
+  d->lpt_hist = (uint32_t *)(b + off[3]);
+  d->lpt = env_flag("RT_LPT", true);
+  {
+    const char *el = getenv("RT_LPT_SPP");
+    d->lpt_spp = (el && *el) ? atoi(el) : 8;
+    if (d->lpt_spp < 1) d->lpt_spp = 1;
+  }
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, d->device));
+  int per_cu = 0;
+  const void *fn = (d->features & ~kFeatBook1) == 0 ? (const void *)rt_general_kernel<kFeatBook1>
+                                                     : (const void *)rt_general_kernel<kFeatAll>;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gen::kBlock, 0));
+  if (per_cu < 1) per_cu = 1;
+  d->gen_grid = prop.multiProcessorCount * per_cu;
+  d->general = true;
+  if (env_flag("RT_DEBUG", false))
+    fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU), features=0x%x\n", d->gen_grid, per_cu,
+            d->features);
+  return 0;
+}
+
 extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) {
   if (s == NULL) {
     rt_set_error("rt_scene_upload: NULL scene");
@@ -759,6 +809,10 @@ extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) 
     rt_scene_release(d);
     return NULL;
   }
+  if (!d->book1 && env_flag("RT_GENERAL", true) && general_upload(d, s) != 0) {
+    rt_scene_release(d);
+    return NULL;
+  }
   return d;
 }
 
@@ -767,6 +821,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   (void)hipSetDevice(d->device);
   (void)hipFree(d->arena);
   if (d->b1_arena) (void)hipFree(d->b1_arena);
+  if (d->gen_arena) (void)hipFree(d->gen_arena);
   for (hipEvent_t e : d->ev_main)
     if (e) (void)hipEventDestroy(e);
   delete d;
@@ -880,6 +935,48 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     }
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
     if (launch_book1(d, V, d_out, st) != 0) return -1;
+    if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+    return 0;
+  }
+  if (d->general) {
+    gen::GeneralView G;
+    G.S = d->view;
+    G.row0 = row0;
+    G.row_stride = row_stride;
+    G.n_rows = n_rows;
+    G.work_counter = d->gen_counter;
+    G.order = nullptr;
+    G.cost_out = nullptr;
+    const bool all = (d->features & ~kFeatBook1) != 0;
+    const dim3 gg((unsigned)d->gen_grid), gb(gen::kBlock);
+    if (d->lpt && G.S.cam.spp >= 4 * d->lpt_spp && npix >= 4096) {  // longest-first order (rays per pixel)
+      gen::GeneralView P = G;
+      P.S.cam.spp = d->lpt_spp;
+      P.cost_out = d->lpt_cost;
+      HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
+      if (all)
+        hipLaunchKernelGGL(rt_general_kernel<kFeatAll>, gg, gb, 0, st, P, d_out);
+      else
+        hipLaunchKernelGGL(rt_general_kernel<kFeatBook1>, gg, gb, 0, st, P, d_out);
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 4096, st));
+      unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);
+      const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+      hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
+      LptModel model;
+      model.spp_ratio = 1.0f;
+      model.grid_waves = d->gen_grid * (gen::kBlock / 64);
+      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, 255, 0, 256, model);
+      hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
+      HIP_OK(hipGetLastError());
+      G.order = d->lpt_order;
+    }
+    HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
+    if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+    if (all)
+      hipLaunchKernelGGL(rt_general_kernel<kFeatAll>, gg, gb, 0, st, G, d_out);
+    else
+      hipLaunchKernelGGL(rt_general_kernel<kFeatBook1>, gg, gb, 0, st, G, d_out);
+    HIP_OK(hipGetLastError());
     if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
     return 0;
   }
@@ -1024,7 +1121,8 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   static thread_local char buf[160];
   if (!d) return "";
   if (!d->book1)
-    snprintf(buf, sizeof buf, "rt_render_rows_kernel<%d>", (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll);
+    snprintf(buf, sizeof buf, "%s<%d>", d->general ? "rt_general_kernel" : "rt_render_rows_kernel",
+             (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll);
   else
     snprintf(buf, sizeof buf, "rt_book1_kernel<%s, %d, %s, %d>", d->book1_lds ? "true" : "false", d->book1_ver,
              d->book1_stats ? "true" : "false", d->book1_occ);
