@@ -51,10 +51,19 @@ static V vcross(V a, V b) { return v(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.
 static V vunit(V a) { return vdivs(a, vlen(a)); }
 
 /* ------------------------------------------------------------------ pcg32 */
+/* ORACLE_COUNT (scripts/cost_model.c only): per-thread event counters for the cost analysis */
+#ifdef ORACLE_COUNT
+static __thread long cnt_draw, cnt_ray, cnt_aabb, cnt_sphere;
+#define COUNT(x) ((x)++)
+#else
+#define COUNT(x) ((void)0)
+#endif
+
 typedef struct {
   uint64_t state, inc;
 } Rng;
 static uint32_t rng_u32(Rng *g) {
+  COUNT(cnt_draw);
   uint64_t old = g->state;
   g->state = old * 6364136223846793005ULL + g->inc;
   uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
@@ -100,6 +109,7 @@ typedef struct {
 static V ray_at(const Ray *r, float t) { return vadd(r->o, vscale(r->d, t)); }
 
 static bool aabb_hit(const rt_bvh_node *n, const Ray *r, float tmin, float tmax) {
+  COUNT(cnt_aabb);
   const float o[3] = {r->o.x, r->o.y, r->o.z}, d[3] = {r->d.x, r->d.y, r->d.z};
   for (int i = 0; i < 3; i++) {
     float inv = 1.0f / d[i];
@@ -118,6 +128,7 @@ static bool aabb_hit(const rt_bvh_node *n, const Ray *r, float tmin, float tmax)
 }
 
 static bool sphere_hit(const rt_sphere *s, const Ray *r, float tmin, float tmax, Rec *rec) {
+  COUNT(cnt_sphere);
   V c = vl(s->center);
   V oc = vsub(r->o, c);
   float a = vdot(r->d, r->d);
@@ -418,6 +429,7 @@ static V light_rand(const rt_flat_scene *S, V origin, Rng *g) {
 /* ------------------------------------------------------------------ ray colour (recursive) */
 static V ray_color(const rt_flat_scene *S, const Ray *r, int depth, Rng *g) {
   if (depth <= 0) return v(0, 0, 0);
+  COUNT(cnt_ray);
   Rec rec;
   if (!hit(S, S->root, r, 1e-3f, INFINITY, &rec, g)) return vl(S->camera.background);
   Ray next = {rec.p, v(0, 0, 0)};
@@ -434,6 +446,9 @@ static V ray_color(const rt_flat_scene *S, const Ray *r, int depth, Rng *g) {
   return vadd(e, vscale(vmul(albedo, ray_color(S, &next, depth - 1, g)), sp / spdf));
 }
 
+#ifdef ORACLE_COUNT
+static __thread long *cnt_trace; /* cumulative (draws incl. the 2 of the seed, rays, boxes, spheres) per sample */
+#endif
 static void pixel(const rt_flat_scene *S, int i, int j, uint8_t *dst) {
   const rt_camera *c = &S->camera;
   Rng g;
@@ -458,6 +473,12 @@ static void pixel(const rt_flat_scene *S, int i, int j, uint8_t *dst) {
     }
     r.d = vadd(vadd(vadd(pos, vscale(du, px)), vscale(dv, py)), vneg(r.o));
     acc = vadd(acc, ray_color(S, &r, c->max_depth, &g));
+#ifdef ORACLE_COUNT
+    if (cnt_trace) {
+      long *q = cnt_trace + 4L * s;
+      q[0] = cnt_draw, q[1] = cnt_ray, q[2] = cnt_aabb, q[3] = cnt_sphere;
+    }
+#endif
   }
   const float ch[3] = {acc.x, acc.y, acc.z};
   for (int k = 0; k < 3; k++) {
@@ -592,3 +613,15 @@ int oracle_dump_flat(const rt_flat_scene *S, const char *path) {
   fclose(f);
   return 0;
 }
+
+#ifdef ORACLE_COUNT
+/* Event counts of pixel (i, j), cumulative after each sample: trace[4*s + {0,1,2,3}] = pcg32 draws
+ * (including the seed's 2), rays, box tests, sphere tests.  Cost analysis only (scripts/cost_model.c). */
+void oracle_count_pixel(const rt_flat_scene *S, int i, int j, long *trace) {
+  uint8_t px[3];
+  cnt_draw = cnt_ray = cnt_aabb = cnt_sphere = 0;
+  cnt_trace = trace;
+  pixel(S, i, j, px);
+  cnt_trace = NULL;
+}
+#endif

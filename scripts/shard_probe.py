@@ -1,6 +1,7 @@
-"""Time one rank's share of the headline frame on one GPU (rows j % world == rank), as bench.py's
+"""Time each rank's share of the headline frame on one GPU (rows j % world == rank), as bench.py's
 N-GPU run would give it; with the RT_* variant knobs in the environment.
-    python scripts/shard_probe.py WORLD [RANK] [SPP]"""
+    python scripts/shard_probe.py WORLDS [RANKS|all] [SPP]      e.g.  2,4,8 all 1000
+The N-GPU frame time is the max over ranks; "scale" is (1-GPU frame time) / (that max)."""
 import os
 import sys
 import time
@@ -9,23 +10,38 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402  (initialised before rtc: see rtc._init_torch_runtime_first)
 import rtc  # noqa: E402
 
-world = int(sys.argv[1])
-rank = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+worlds = [int(w) for w in sys.argv[1].split(",")]
+ranks_arg = sys.argv[2] if len(sys.argv) > 2 else "0"
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
 sc = rtc.Scene.preset(1, 1200, spp, 50)
-row0, stride, n = rtc.rows_of(sc.height, rank, world)
 ds = rtc.DeviceScene(sc, 0)
-buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream()
-ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)  # warm-up
-torch.cuda.synchronize()
-times = []
-for _ in range(2):
-    t0 = time.perf_counter()
-    ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)
+
+
+def time_rows(row0, stride, n, reps=2):
+    buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda")
+    ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)  # warm-up
     torch.cuda.synchronize()
-    times.append(time.perf_counter() - t0)
-t = min(times)
-print(f"world={world} rank={rank} rows={n} ms={t * 1e3:.1f} kernel_ms={ds.last_launch_ms():.1f} "
-      f"frame_Msamples/s_if_all_ranks_equal={sc.width * sc.height * spp / t / 1e6:.0f}", flush=True)
+    best, kbest = 1e30, 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+        kbest = min(kbest, ds.last_launch_ms())
+    return best, kbest
+
+
+t1, k1 = time_rows(0, 1, sc.height)
+print(f"world=1 ms={t1 * 1e3:.1f} kernel_ms={k1:.1f} Msamples/s={sc.width * sc.height * spp / t1 / 1e6:.0f}", flush=True)
+for world in worlds:
+    ranks = range(world) if ranks_arg == "all" else [int(r) for r in ranks_arg.split(",")]
+    worst = 0.0
+    for rank in ranks:
+        row0, stride, n = rtc.rows_of(sc.height, rank, world)
+        t, k = time_rows(row0, stride, n)
+        worst = max(worst, t)
+        print(f"  world={world} rank={rank} rows={n} ms={t * 1e3:.1f} kernel_ms={k:.1f}", flush=True)
+    print(f"world={world} max_ms={worst * 1e3:.1f} frame_Msamples/s={sc.width * sc.height * spp / worst / 1e6:.0f} "
+          f"scale={t1 / worst:.2f}x", flush=True)
 ds.close()
