@@ -66,6 +66,10 @@ struct Book1View {
   const float4 *items9_g;    // v9: the world in traversal preorder, 2 float4 per item (Item9 below)
   int32_t n_items9, n_items9_alloc;  // items, and items incl. the zero pad item at the end
   int32_t spill_lanes;
+  int32_t n_bf_leaves;       // whole-wave pixels: leaves for bf_trace; 0: off (coop_trace9 instead)
+  uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end}, wall_clock64 low bits
+  const uint4 *wide;         // group trace (rt_group.h): 8-entry treelets over the preorder items
+  int32_t n_wide;            // 0: group kernel unavailable for this scene
 };
 
 // ---------------------------------------------------------------- wave helpers
@@ -984,6 +988,90 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const Lane &L, in
   out_hit = hit;
 }
 
+// ---------------------------------------------------------------- whole-wave closest hit by candidates
+// The reference's traversal (preorder visit, box culling against the shrinking t_max) returns the
+// first-visited sphere of least accepted root.  A sphere's accepted root r (q1, or q2 when q1 <= t_min:
+// see above) does not depend on t_max, so take s* = the leaf of least valid r (t_min < r < inf),
+// earliest in preorder among equal r.  Every sphere visited before s* is earlier in preorder, so its
+// root is > r*, and the t_max at each of s*'s ancestors' visits is > r*.  An ancestor box is then
+// entered (!(fminf(t_max, X) <= E), monotone in t_max) whenever fminf(r*, X) > E; if that holds for
+// all of s*'s ancestors, s* is visited, accepted (t_max > r* at its visit) and never displaced (no
+// root is smaller, equal roots later in preorder fail r >= t_max): the reference returns (r*, s*).
+// If the ancestor check fails (a grazing box) or a root is NaN, the exact scan (coop_trace9) runs.
+// A miss (no valid root at all) is exact: the reference cannot accept anything.
+// Cost per ray, all from LDS: kBfSlots sphere roots per lane (the square root and divisions only
+// where some lane's discriminant is >= 0), a 6-step wave argmin, and the ancestor check: the nodes
+// q < p* with p* < q + skip(q), found by the lanes among all items before p* -- instead of a ~50-item
+// sequential scan whose every decision is a VALU -> scalar round trip.
+constexpr int kBfSlots = 8;  // 64 x 8 = 512 leaves at most (host-checked)
+
+RT_D void box_interval(float4 q0, float4 q1, const CoopRay &C, float tmin, float &e, float &x) {
+  const float t0x = (q0.x - C.ox) * C.ix, t1x = (q0.y - C.ox) * C.ix;
+  const float t0y = (q0.z - C.oy) * C.iy, t1y = (q0.w - C.oy) * C.iy;
+  const float t0z = (q1.x - C.oz) * C.iz, t1z = (q1.y - C.oz) * C.iz;
+  const float nx = C.ix < 0 ? t1x : t0x, fx = C.ix < 0 ? t0x : t1x;
+  const float ny = C.iy < 0 ? t1y : t0y, fy = C.iy < 0 ? t0y : t1y;
+  const float nz = C.iz < 0 ? t1z : t0z, fz = C.iz < 0 ? t0z : t1z;
+  e = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+  x = fminf(fminf(fx, fy), fz);
+}
+
+// Leaf n's item position is kept in a spare word of item n (q1.w of a node item, q1.x of a leaf
+// item; host: book1_upload), so the per-ray sphere reads need no table and no registers held across
+// the pixel (held spheres would raise the whole kernel's VGPR count and cut the lane waves'
+// occupancy).  Returns false when the candidate check cannot decide; the caller then runs the
+// exact scan.  Split in two so that the caller can start the hit sphere's material load before the
+// ancestor check: bf_candidate returns false (undecided: a NaN root) or the candidate (r*, p*);
+// p* = -1 for a miss; bf_verify is the ancestor check of a candidate p* >= 0.
+RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
+                       int &out_bp) {
+  const int lane = __lane_id();
+  float best = __builtin_inff();
+  int bp = 0x7fffffff;  // item position of the best leaf (preorder rank)
+  bool nan = false;
+#pragma unroll 2
+  for (int k = 0; k < kBfSlots; k++) {
+    if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
+    const int n = k * 64 + lane;
+    const bool live = n < V.n_bf_leaves;
+    const float4 h = items[2 * (live ? n : 0) + 1];
+    const uint32_t hw = __float_as_uint(h.w);
+    const int pos = (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw);
+    const float r = coop_sphere_root(items[2 * pos], C, tmin);
+    nan |= live && r != r;
+    if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {  // argmin over (root, preorder position)
+    const float ob = __shfl_xor(best, off);
+    const int op = __shfl_xor(bp, off);
+    if (ob < best || (ob == best && op < bp)) best = ob, bp = op;
+  }
+  if (__ballot(nan) != 0) return false;
+  out_best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(best)));
+  bp = __builtin_amdgcn_readfirstlane(bp);
+  out_bp = bp == 0x7fffffff ? -1 : bp;  // no valid root anywhere: a miss
+  return true;
+}
+
+RT_D bool bf_verify(const float4 *items, const CoopRay &C, float tmin, float best, int bp) {
+  const int lane = __lane_id();
+  bool bad = false;
+  for (int base = 0; base < bp; base += 64) {  // wave-uniform bound
+    const int q = base + lane;
+    if (q < bp) {
+      const float4 q1 = items[2 * q + 1];
+      const uint32_t w = __float_as_uint(q1.w);
+      if (!(w & kLeaf9) && (uint32_t)bp < (uint32_t)q + __float_as_uint(q1.z)) {  // an ancestor of p*
+        float e, x;
+        box_interval(items[2 * q], q1, C, tmin, e, x);
+        bad |= !(fminf(best, x) > e);
+      }
+    }
+  }
+  return __ballot(bad) == 0;
+}
+
 // A whole pixel (all its samples, in order) rendered by one wave: the path state is wave-uniform
 // (every lane holds the same values and runs the same shading), and each ray is traced with
 // coop_trace9.  For the few pixels whose sequential chain is far longer than the frame's fair share
@@ -1006,6 +1094,8 @@ RT_D void render_pixel_coop(const Book1View &V, const float4 *items9, int64_t pi
   L.cur = 0;
   L.pend0 = L.pend1 = 0xffffu;
   L.sp = L.k = 0;
+  const bool use_bf = V.n_bf_leaves > 0;
+  const uint32_t px_start = V.px_time ? (uint32_t)wall_clock64() : 0u;
   for (int s = 0; s < cam.spp; s++) {
     // camera ray (src/raytracing.c:96-122)
     const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
@@ -1022,39 +1112,99 @@ RT_D void render_pixel_coop(const Book1View &V, const float4 *items9, int64_t pi
       o = add(add(lf, scale(ld3(cam.disc_u), a)), scale(ld3(cam.disc_v), b));
     }
     f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
-    Record R;
-    R.r0 = R.r1 = 0;
-    R.n = 0;
+    // the path record lives in the lanes: lane k holds the albedo of bounce k (max_depth <= 64)
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+    int n_b = 0;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     for (int depth = cam.max_depth; depth > 0;) {  // Camera_ray_color (src/raytracing.c:39-75)
-      L.ox = o.x, L.oy = o.y, L.oz = o.z;
-      L.dx = d.x, L.dy = d.y, L.dz = d.z;
-      L.ix = 1.0f / d.x, L.iy = 1.0f / d.y, L.iz = 1.0f / d.z;
-      L.a = dot(d, d);
-      L.fast = L.a >= kDivLo && L.a <= kDivHi;
-      L.ra = recip_core(L.a);
-      float tmax;
-      int hit;
-      coop_trace9(V, items9, L, 0, tmin, tmax, hit);
-      if (hit < 0) {
+      CoopRay C;
+      C.ox = o.x, C.oy = o.y, C.oz = o.z, C.dx = d.x, C.dy = d.y, C.dz = d.z;
+      C.ix = 1.0f / d.x, C.iy = 1.0f / d.y, C.iz = 1.0f / d.z;
+      C.a = dot(d, d);
+      C.fast = C.a >= kDivLo && C.a <= kDivHi;
+      C.ra = recip_core(C.a);
+      float tmax = __builtin_inff();
+      int bp = -1;
+      bool decided = use_bf && bf_candidate(V, items9, C, tmin, tmax, bp);
+      // the hit sphere (center, 1/r, material) from its LDS item, and its material's load issued
+      // before the ancestor check so that its latency overlaps it
+      float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
+      FastMat m;
+      if (decided && bp >= 0) {
+        s0 = items9[2 * bp], s1 = items9[2 * bp + 1];
+        m = V.mats[__float_as_int(s1.z)];
+        decided = bf_verify(items9, C, tmin, tmax, bp);
+      }
+      if (!decided) {  // the exact scan
+        L.ox = C.ox, L.oy = C.oy, L.oz = C.oz, L.dx = C.dx, L.dy = C.dy, L.dz = C.dz;
+        L.ix = C.ix, L.iy = C.iy, L.iz = C.iz, L.a = C.a, L.ra = C.ra, L.fast = C.fast;
+        int hit;
+        coop_trace9(V, items9, L, 0, tmin, tmax, hit);
+        bp = hit;
+        if (hit >= 0) {
+          const rt_sphere &sp = V.S.spheres[hit];
+          s0 = make_float4(sp.center[0], sp.center[1], sp.center[2], 0.0f);
+          s1 = make_float4(0.0f, sp.inv_radius, __int_as_float(sp.material), 0.0f);
+          m = V.mats[sp.material];
+        }
+      }
+      if (bp < 0) {
         tail = ld3(cam.background);
         break;
       }
-      const rt_sphere &sp = V.S.spheres[hit];
       const f3 p = ray_at(o, d, tmax);
-      const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
+      const f3 outward = scale(sub(p, mk(s0.x, s0.y, s0.z)), s1.y);
       const bool front = dot(d, outward) < 0.0f;
       const f3 normal = front ? outward : neg(outward);
-      const FastMat &m = V.mats[sp.material];
       const f3 nd = scatter(m, normal, front, d, g);
-      rec_push(V, R, (uint32_t)sp.material, glane);
+      if (__lane_id() == n_b) ar = m.albedo[0], ag = m.albedo[1], ab = m.albedo[2];
+      n_b++;
       o = p;
       d = nd;
       depth--;
     }
-    acc = add(acc, rec_fold(V, R, tail, glane));
+    // fold innermost first, as the recursion returns: c = 0 + a_k (x) c (rec_fold_chunk)
+    f3 c = tail;
+    for (int k = n_b - 1; k >= 0; k--) {
+      const f3 a = mk(lane_bcast(ar, k), lane_bcast(ag, k), lane_bcast(ab, k));
+      c = add(mk(0.0f, 0.0f, 0.0f), mul(a, c));
+    }
+    acc = add(acc, c);
   }
-  if (__lane_id() == 0) write_pixel(out + pix * 3, acc, cam.spp);
+  if (__lane_id() == 0) {
+    write_pixel(out + pix * 3, acc, cam.spp);
+    if (V.px_time) V.px_time[2 * pix] = px_start, V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+  }
+}
+
+// The whole-wave kernel (rt_book1_wave_kernel), launched on a second stream next to the lane kernel:
+// its first *coop_waves_dev waves claim the first *n_coop items of the order, one pixel per wave,
+// heaviest first.  A kernel of its own, so that the whole-wave code's registers do not count
+// against the lane kernel's occupancy; the lane kernel leaves it the same number of workgroups.
+template <bool kLds>
+__device__ void render_wave_items(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
+  const int waves = (int)*V.coop_waves_dev;
+  if ((int)blockIdx.x * kWaves >= waves) return;  // whole workgroup: before the barrier
+  float4 *items9 = (float4 *)lds;
+  if (kLds) {
+    for (int q = threadIdx.x; q < 2 * V.n_items9_alloc; q += kBlock) items9[q] = V.items9_g[q];
+    __syncthreads();
+  } else {
+    items9 = (float4 *)V.items9_g;
+  }
+  const int wave = (int)(blockIdx.x * kBlock + threadIdx.x) / 64;
+  if (wave >= waves) return;
+  const int64_t n_coop = (int64_t)*V.n_coop;
+  const int glane = (int)(blockIdx.x * kBlock + threadIdx.x);
+  for (;;) {
+    int k = 0;
+    if (__lane_id() == 0) k = atomicAdd(V.coop_counter, 1);
+    k = __shfl(k, 0);
+    if (k >= n_coop) break;
+    __builtin_amdgcn_s_setprio(3);  // these chains set the frame time: issue before the lane-parallel waves
+    render_pixel_coop(V, items9, (int64_t)V.order[k], out, glane);
+    __builtin_amdgcn_s_setprio(0);
+  }
 }
 
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
@@ -1066,6 +1216,9 @@ constexpr int kSteps = 4;
 template <bool kLds, bool kStats = false, int kStep = 5>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
+  // the last workgroups of the grid leave their CU slots to the whole-wave kernel (render_wave_items)
+  if (V.n_coop != nullptr && (int)blockIdx.x >= (int)gridDim.x - (int)((*V.coop_waves_dev + kWaves - 1) / kWaves))
+    return;
   const int W = V.S.cam.width;
   const int64_t total = (int64_t)V.n_rows * W;
   // LDS: nodes (lo.x hi.x lo.y hi.y | lo.z hi.z left right) + spheres, then the 16-bit stacks
@@ -1138,23 +1291,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   L.pend0 = L.pend1 = 0xffffu;
   L.sp = L.k = 0;
 
-  // the heaviest pixels first, one per wave (render_pixel_coop), on the grid's first coop_waves waves
-  int64_t work_offset = 0;  // the lanes' own items start after the cooperative ones
-  if (kStep == 9 && kLds && V.n_coop != nullptr) {
-    const int64_t n_coop = (int64_t)*V.n_coop;
-    work_offset = n_coop;
-    if (glane / 64 < (int)*V.coop_waves_dev) {
-      for (;;) {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(V.coop_counter, 1);
-        k = __shfl(k, 0);
-        if (k >= n_coop) break;
-        __builtin_amdgcn_s_setprio(3);  // these chains set the frame time: issue before the lane-parallel waves
-        render_pixel_coop(V, items9, (int64_t)V.order[k], out, glane);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-  }
+  // the heaviest items (the first *n_coop of the order) are rendered by whole waves in the concurrent
+  // rt_book1_wave_kernel (render_wave_items); the lanes' own items start after them
+  const int64_t work_offset = V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   const int64_t total_own = total - work_offset;
   const int64_t n_heavy = (V.order && V.n_heavy) ? (int64_t)*V.n_heavy : 0;
   bool heavy = false;  // this lane's pixel is among the n_heavy longest
@@ -1279,6 +1418,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (s == spp) {  // quantize (src/raytracing.c:127-131)
           write_pixel(out + pix * 3, acc, spp);
           if (V.cost_out) V.cost_out[pix] = px_steps;
+          if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kStats) {
             V.pixel_cost[2 * pix] = px_steps;
             V.pixel_cost[2 * pix + 1] = (uint32_t)((long long)wall_clock64() - px_t0);
@@ -1313,6 +1453,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         s = 0;
         need_pixel = false;
         px_steps = 0;
+        if (V.px_time) V.px_time[2 * pix] = (uint32_t)wall_clock64();
         if (kStats) px_t0 = (long long)wall_clock64();
       }
       // camera ray (src/raytracing.c:96-122)

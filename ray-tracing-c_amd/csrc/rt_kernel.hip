@@ -21,6 +21,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_book1.h"
+#include "rt_group.h"
 #include "rt_general.h"
 #include "rt_device.h"
 
@@ -70,6 +71,21 @@ __global__ __launch_bounds__(b1::kBlock, kOcc > 0 ? kOcc : 1) void rt_book1_kern
     b1::render_batched<kLds, kStats, kVer>(V, out, lds);
   else
     b1::render<kLds>(V, out, lds);
+}
+
+// The group kernel (rt_group.h): eight lanes per pixel, for frames with few pixels per lane.
+template <bool kLds>
+__global__ __launch_bounds__(grp::kBlock) void rt_book1_group_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  grp::render_groups<kLds>(V, out, lds);
+}
+
+// The whole-wave items of a Book-1 launch (rt_book1.h: render_wave_items), concurrent with the lane
+// kernel on a second stream.
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock) void rt_book1_wave_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  b1::render_wave_items<kLds>(V, out, lds);
 }
 
 // The LPT cost pre-pass: the same persistent kernel at low spp, under its own name so profiles
@@ -311,6 +327,12 @@ struct rt_device_scene {
   int gen_grid = 0;
   int b1_grid = 0;
   size_t b1_lds_bytes = 0;
+  uint32_t *px_time = nullptr;  // RT_PX_TIME diagnostic: {start, end} per work item
+  int group_mode = 2;                 // RT_MODE: 0 lane kernel, 1 group kernel, 2 auto (by pixels per lane)
+  int g_grid = 0;                     // group kernel: resident workgroups, LDS bytes per workgroup
+  size_t g_lds_bytes = 0;
+  hipStream_t wave_stream = nullptr;  // the whole-wave kernel's stream (forked from / joined to the caller's)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -515,14 +537,19 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   }
   // v9 items (rt_book1.h: trav_step_v9): the root list's hittables in traversal preorder
   std::vector<float4> items9;
+  std::vector<uint32_t> bf_item;  // whole-wave candidate trace (rt_book1.h: bf_trace): leaf item positions
   {
     std::function<void(int32_t)> emit = [&](int32_t ref) {
       if (ref == RT_REF_NONE) return;
       const int32_t i = rt_ref_index(ref);
       if (rt_ref_kind(ref) == RT_KIND_SPHERE) {
         const rt_sphere &sp = s->spheres[i];
-        items9.push_back(make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius_sq));
-        items9.push_back(make_float4(0.0f, 0.0f, 0.0f, bits_as_float((uint32_t)i | b1::kLeaf9)));
+        const float4 c = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius_sq);
+        items9.push_back(c);
+        // (x: bf_trace position slot, y: 1/r and z: material for the whole-wave shading, w: index)
+        items9.push_back(make_float4(0.0f, sp.inv_radius, bits_as_float((uint32_t)sp.material),
+                                     bits_as_float((uint32_t)i | b1::kLeaf9)));
+        bf_item.push_back((uint32_t)(items9.size() / 2 - 1));
         return;
       }
       const rt_bvh_node &n = s->bvh[i];
@@ -537,6 +564,91 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     // one zero item past the end: the step reads its successor before knowing it exists
     items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  }
+  // bf_trace: leaf n's item position in a spare word of item n (q1.w of a node, q1.x of a leaf)
+  for (size_t n = 0; n < bf_item.size() && 2 * n + 1 < items9.size(); n++) {
+    float4 &h = items9[2 * n + 1];
+    uint32_t hw;
+    memcpy(&hw, &h.w, 4);
+    if (hw & b1::kLeaf9)
+      h.x = bits_as_float(bf_item[n]);
+    else
+      h.w = bits_as_float(bf_item[n]);
+  }
+  // group trace treelets (rt_group.h): greedy 8-entry treelets over the preorder items, each entry
+  // with up to 3 intermediate nodes between it and the treelet's (already tested) root
+  std::vector<uint4> wide;
+  {
+    const int n_items = (int)(items9.size() / 2) - 1;  // without the pad item
+    auto is_leaf = [&](int p) {
+      uint32_t w;
+      memcpy(&w, &items9[2 * p + 1].w, 4);
+      return (w & b1::kLeaf9) != 0;
+    };
+    auto size_of = [&](int p) {
+      if (is_leaf(p)) return 1;
+      uint32_t k;
+      memcpy(&k, &items9[2 * p + 1].z, 4);
+      return (int)k;
+    };
+    auto kids = [&](int p, int out[2]) {
+      const int l = p + 1;
+      int n = 0;
+      out[n++] = l;
+      if (l + size_of(l) < p + size_of(p)) out[n++] = l + size_of(l);
+      return n;
+    };
+    struct E {
+      int item, n_inter, inter[3];
+    };
+    bool ok = n_items > 0 && n_items < 0xffff;
+    std::function<int(const std::vector<int> &)> make = [&](const std::vector<int> &level1) -> int {
+      if (!ok || level1.size() > (size_t)grp::kG) return ok = false, -1;
+      std::vector<E> es;
+      for (int c : level1) es.push_back({c, 0, {0, 0, 0}});
+      for (;;) {  // open the internal entry with the largest subtree while the treelet has room
+        int pick = -1;
+        for (int k = 0; k < (int)es.size(); k++) {
+          int kc[2];
+          if (is_leaf(es[k].item) || es[k].n_inter >= 3 || (int)es.size() + kids(es[k].item, kc) - 1 > grp::kG)
+            continue;
+          if (pick < 0 || size_of(es[k].item) > size_of(es[pick].item)) pick = k;
+        }
+        if (pick < 0) break;
+        const E old = es[pick];
+        int kc[2];
+        const int nc = kids(old.item, kc);
+        std::vector<E> repl;
+        for (int c = 0; c < nc; c++) {
+          E e = old;
+          e.item = kc[c];
+          e.inter[e.n_inter++] = old.item;
+          repl.push_back(e);
+        }
+        es.erase(es.begin() + pick);
+        es.insert(es.begin() + pick, repl.begin(), repl.end());
+      }
+      const int id = (int)(wide.size() / grp::kG);
+      for (int k = 0; k < grp::kG; k++) wide.push_back(make_uint4(grp::kEmpty, 0u, 0u, 0u));
+      for (int k = 0; k < (int)es.size(); k++) {
+        const E &e = es[k];
+        uint32_t child = 0;
+        if (!is_leaf(e.item)) {
+          int kc[2];
+          const int nc = kids(e.item, kc);
+          const int c = make(std::vector<int>(kc, kc + nc));
+          if (c < 0) return -1;
+          child = (uint32_t)c;
+        }
+        wide[(size_t)id * grp::kG + k] =
+            make_uint4((uint32_t)e.item, child, (uint32_t)e.inter[0] | (uint32_t)e.inter[1] << 16,
+                       (uint32_t)e.inter[2] | (uint32_t)e.n_inter << 16);
+      }
+      return id;
+    };
+    std::vector<int> tops;
+    for (int p = 0; p < n_items; p += size_of(p)) tops.push_back(p);
+    if (make(tops) != 0 || !ok) wide.clear();
   }
   std::vector<float4> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++)
@@ -613,16 +725,17 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth / 4) * spill_lanes * sizeof(uint64_t);  // Record chunks
 
-  size_t off[13], total = 0;
+  size_t off[14], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[13] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+  const size_t sizes[14] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
                            roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
                            nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t),
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
-                           4096};                                                            // [12] LPT buckets
-  for (int k = 0; k < 13; k++) {
+                           4096,                                                             // [12] LPT buckets
+                           wide.size() * sizeof(uint4)};                                     // [13] treelets
+  for (int k = 0; k < 14; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -636,6 +749,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   HIP_OK(hipMemcpy(b + off[7], nodes7.data(), sizes[7], hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(b + off[8], roots7.data(), sizes[8], hipMemcpyHostToDevice));
   if (sizes[9]) HIP_OK(hipMemcpy(b + off[9], items9.data(), sizes[9], hipMemcpyHostToDevice));
+  if (sizes[13]) HIP_OK(hipMemcpy(b + off[13], wide.data(), sizes[13], hipMemcpyHostToDevice));
   d->b1_arena = arena;
   b1::Book1View &V = d->b1view;
   V.S = d->view;
@@ -651,6 +765,37 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.root7_items = (const uint16_t *)(b + off[8]);
   V.n_nodes7 = (int32_t)(nodes7.size() / 4);
   V.items9_g = (const float4 *)(b + off[9]);
+  V.wide = (const uint4 *)(b + off[13]);
+  V.n_wide = (int32_t)(wide.size() / grp::kG);
+  {  // the group kernel (rt_group.h), for frames with few pixels per lane
+    const char *em = getenv("RT_MODE");
+    d->group_mode = (em && !strcmp(em, "lane")) ? 0 : (em && !strcmp(em, "group")) ? 1 : 2;
+    if (V.n_wide == 0 || d->book1_ver != 9 || d->book1_stats) d->group_mode = 0;
+    if (d->group_mode != 0) {
+      const bool lds = d->book1_lds;
+      d->g_lds_bytes = align_up((lds ? items9.size() * sizeof(float4) : 0) +
+                                    (size_t)grp::kGroups * grp::kStack * sizeof(uint2), 16);
+      int per = 0;
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per, lds ? (const void *)rt_book1_group_kernel<true> : (const void *)rt_book1_group_kernel<false>,
+          grp::kBlock, d->g_lds_bytes));
+      d->g_grid = prop.multiProcessorCount * (per < 1 ? 1 : per);
+      if (d->g_grid * grp::kGroups > spill_lanes) d->g_grid = spill_lanes / grp::kGroups;  // record spill columns
+    }
+  }
+  if (d->book1_ver == 9 && !d->book1_stats) {  // whole-wave items run concurrently on a second stream
+    HIP_OK(hipStreamCreateWithFlags(&d->wave_stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+  }
+  V.px_time = nullptr;
+  if (env_flag("RT_PX_TIME", false)) {
+    HIP_OK(hipMalloc(&d->px_time, (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t)));
+    V.px_time = d->px_time;
+  }
+  // whole-wave pixels trace by candidates (bf_trace) when every leaf fits the wave's slots
+  V.n_bf_leaves = !bf_item.empty() && bf_item.size() <= (size_t)64 * b1::kBfSlots && env_flag("RT_BF", true)
+                      ? (int32_t)bf_item.size() : 0;
   d->lpt_cost = (uint32_t *)(b + off[10]);
   d->lpt_order = (int32_t *)(b + off[11]);
   d->lpt_hist = (uint32_t *)(b + off[12]);
@@ -822,6 +967,10 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   (void)hipFree(d->arena);
   if (d->b1_arena) (void)hipFree(d->b1_arena);
   if (d->gen_arena) (void)hipFree(d->gen_arena);
+  if (d->px_time) (void)hipFree(d->px_time);
+  if (d->wave_stream) (void)hipStreamDestroy(d->wave_stream);
+  if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+  if (d->ev_join) (void)hipEventDestroy(d->ev_join);
   for (hipEvent_t e : d->ev_main)
     if (e) (void)hipEventDestroy(e);
   delete d;
@@ -894,6 +1043,10 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     V.row0 = row0;
     V.row_stride = row_stride;
     V.n_rows = n_rows;
+    // the group kernel when the launch has fewer pixels than the lane kernel has lanes (a frame split
+    // over several GPUs): there the sequential per-pixel chains, not the lanes' throughput, set the time
+    const bool use_group =
+        d->group_mode == 1 || (d->group_mode == 2 && npix < (int64_t)d->b1_grid * b1::kBlock);
     // longest-first order: a low-spp pass measures each work item's traversal steps
     if (d->lpt && V.S.cam.spp >= 4 * d->lpt_spp && npix >= 4096) {
       b1::Book1View P = V;
@@ -927,14 +1080,41 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
         fprintf(stderr, "[rtc] lpt: %lld items, %u cooperative on %u waves (RT_COOP_STEPS %d, RT_COOP_WAVES %d; <0: "
                 "model), %u at raised priority\n", (long long)npix, nc, nw, d->coop_steps, d->coop_waves, nh);
       }
-      if (d->coop_waves != 0) {
+      if (d->coop_waves != 0 && d->wave_stream && !use_group) {
         V.n_coop = d->lpt_hist + 512;
         V.coop_counter = (int32_t *)(d->lpt_hist + 513);
         V.coop_waves_dev = d->lpt_hist + 515;
       }
     }
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+    if (use_group) {  // eight lanes per pixel (rt_group.h)
+      HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+      const dim3 gg((unsigned)d->g_grid), gb(grp::kBlock);
+      if (d->book1_lds)
+        hipLaunchKernelGGL((rt_book1_group_kernel<true>), gg, gb, d->g_lds_bytes, st, V, d_out);
+      else
+        hipLaunchKernelGGL((rt_book1_group_kernel<false>), gg, gb, d->g_lds_bytes, st, V, d_out);
+      HIP_OK(hipGetLastError());
+      if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+      return 0;
+    }
+    const bool split = V.n_coop != nullptr;
+    if (split) {  // whole-wave items: a concurrent kernel on the second stream (rt_book1.h: render_wave_items)
+      HIP_OK(hipEventRecord(d->ev_fork, st));
+      HIP_OK(hipStreamWaitEvent(d->wave_stream, d->ev_fork, 0));
+      // as many workgroups as the model may give it; the lane kernel leaves it that many CU slots
+      const dim3 gw((unsigned)(d->b1_grid / 2 > 0 ? d->b1_grid / 2 : 1)), blk(b1::kBlock);
+      if (d->book1_lds)
+        hipLaunchKernelGGL((rt_book1_wave_kernel<true>), gw, blk, d->b1_lds_bytes, d->wave_stream, V, d_out);
+      else
+        hipLaunchKernelGGL((rt_book1_wave_kernel<false>), gw, blk, d->b1_lds_bytes, d->wave_stream, V, d_out);
+      HIP_OK(hipGetLastError());
+    }
     if (launch_book1(d, V, d_out, st) != 0) return -1;
+    if (split) {
+      HIP_OK(hipEventRecord(d->ev_join, d->wave_stream));
+      HIP_OK(hipStreamWaitEvent(st, d->ev_join, 0));
+    }
     if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
     return 0;
   }
@@ -1113,6 +1293,22 @@ extern "C" int rt_book1_pixel_cost(rt_device_scene *d, uint32_t *out, int64_t n_
   HIP_OK(hipSetDevice(d->device));
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemcpy(out, d->b1view.pixel_cost, (size_t)n_items * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int rt_scene_px_time(rt_device_scene *d, uint32_t *times, uint32_t *cost, int32_t *order,
+                                uint32_t *n_coop, int64_t n) {
+  if (!d || !d->book1) return rt_set_error("rt_scene_px_time: not a Book-1 scene"), -1;
+  if (n < 0 || n > (int64_t)d->width * d->height) return rt_set_error("rt_scene_px_time: bad count"), -1;
+  HIP_OK(hipSetDevice(d->device));
+  HIP_OK(hipDeviceSynchronize());
+  if (times) {
+    if (!d->px_time) return rt_set_error("rt_scene_px_time: upload with RT_PX_TIME=1"), -1;
+    HIP_OK(hipMemcpy(times, d->px_time, (size_t)n * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  if (cost) HIP_OK(hipMemcpy(cost, d->lpt_cost, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (order) HIP_OK(hipMemcpy(order, d->lpt_order, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (n_coop) HIP_OK(hipMemcpy(n_coop, d->lpt_hist + 512, sizeof(uint32_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

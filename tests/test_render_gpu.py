@@ -140,7 +140,11 @@ def test_cli_rt_main_matches_golden(manifest, tmp_path):
 
 
 @pytest.mark.parametrize("env", [{"RT_BOOK1": "0"}, {"RT_BOOK1": "0", "RT_GENERAL": "0"}, {"RT_BOOK1_LDS": "0"}, {}, {"RT_BOOK1_V": "2"},
-                                 {"RT_BOOK1_V": "3"}, {"RT_BOOK1_V": "5"}, {"RT_BOOK1_V": "6"}, {"RT_BOOK1_V": "7"}, {"RT_BOOK1_V": "9"}, {"RT_BOOK1_V": "9", "RT_BOOK1_LDS": "0"}, {"RT_BOOK1_V": "9", "RT_COOP_LANES": "64"}, {"RT_BOOK1_V": "5", "RT_COOP_LANES": "64"}, {"RT_BOOK1_STATS": "1"}, {"RT_LPT": "0"}, {"RT_LPT_SPP": "1"}, {"RT_COOP_STEPS": "50"}, {"RT_COOP_WAVES": "0"}, {"RT_COOP_LANES": "64"}, {"RT_COOP_LANES": "0"}, {"RT_SHADE_BATCH": "1"},
+                                 {"RT_BOOK1_V": "3"}, {"RT_BOOK1_V": "5"}, {"RT_BOOK1_V": "6"}, {"RT_BOOK1_V": "7"}, {"RT_BOOK1_V": "9"}, {"RT_BOOK1_V": "9", "RT_BOOK1_LDS": "0"}, {"RT_BOOK1_V": "9", "RT_COOP_LANES": "64"}, {"RT_BOOK1_V": "5", "RT_COOP_LANES": "64"}, {"RT_BOOK1_STATS": "1"}, {"RT_LPT": "0"}, {"RT_LPT_SPP": "1"}, {"RT_COOP_STEPS": "50"}, {"RT_COOP_WAVES": "0"},
+                                 {"RT_MODE": "lane"}, {"RT_MODE": "group"}, {"RT_MODE": "group", "RT_BOOK1_LDS": "0"},
+                                 {"RT_MODE": "group", "RT_LPT": "0"}, {"RT_MODE": "lane", "RT_LPT_SPP": "1"},
+                                 {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024"},
+                                 {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024", "RT_BF": "0"}, {"RT_COOP_LANES": "64"}, {"RT_COOP_LANES": "0"}, {"RT_SHADE_BATCH": "1"},
                                  {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"}])
 @pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
 def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
