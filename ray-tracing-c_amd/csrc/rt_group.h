@@ -136,6 +136,12 @@ RT_D bool group_trace(const b1::Book1View &V, const float4 *items, uint2 *stk, c
 template <bool kLds>
 __device__ void render_groups(const b1::Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
+  // as the lane kernel: the last workgroups leave their slots to the whole-wave kernel, and the
+  // groups' items start after the whole-wave ones (rt_book1.h: render_wave_items)
+  if (V.n_coop != nullptr &&
+      (int)blockIdx.x >= (int)gridDim.x - (int)((*V.coop_waves_dev + b1::kWaves - 1) / b1::kWaves))
+    return;
+  const int64_t work_offset = V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   float4 *items = (float4 *)lds;
   uint2 *stacks = (uint2 *)(items + (kLds ? 2 * V.n_items9_alloc : 0));
   if (kLds) {
@@ -150,7 +156,7 @@ __device__ void render_groups(const b1::Book1View &V, uint8_t *__restrict__ out,
   const int spill_lane = (int)(blockIdx.x * kBlock + tid) / kG;  // one record spill column per group
   const rt_camera &cam = V.S.cam;
   const int W = cam.width;
-  const int64_t total = (int64_t)V.n_rows * W;
+  const int64_t total = (int64_t)V.n_rows * W - work_offset;
   const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
   const float tmin = 1e-3f;
   bool alive = true, need_pixel = true;
@@ -177,7 +183,7 @@ __device__ void render_groups(const b1::Book1View &V, uint8_t *__restrict__ out,
         if (k >= total) {
           alive = false;
         } else {
-          pix = V.order ? (int64_t)V.order[k] : k;
+          pix = V.order ? (int64_t)V.order[k + work_offset] : k;
           const int jj = (int)(pix / W);
           i = (int)(pix - (int64_t)jj * W);
           j = V.row0 + jj * V.row_stride;

@@ -237,11 +237,23 @@ __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist, uns
 // traversal step per kDfsStep clocks, the lanes together at kDfsUse of that rate; a whole-wave
 // pixel costs kCoopStep clocks per step.  The frame ends when both the slowest lane pixel and the
 // whole-wave queue are done.
+// LPT scratch: 256 bucket counts, 256 running offsets, 4 split counters (u32 [512..515]), then from
+// u32 544 the 256 per-bucket step sums (u64): 2176 + 2048 bytes
+constexpr size_t kLptHistBytes = 8192;
+
 struct LptModel {
   float spp_ratio;  // frame spp / pre-pass spp (costs are pre-pass steps)
   int grid_waves;
+  float dfs_step;   // clocks per step of a lane (or group) pixel under load
+  float dfs_use;    // the lanes' (groups') aggregate rate, as a fraction of dfs_step per lane (group)
+  float coop_step;  // clocks per step of a whole-wave pixel
+  int lanes_per_wave;  // pixels in flight per non-cooperative wave: 64 lanes, or 8 groups
+  int debug;           // RT_DEBUG: print the model's inputs and choice
 };
-constexpr float kDfsStep = 1700.0f, kDfsUse = 0.7f, kCoopStep = 400.0f;
+// measured on the headline frame (scripts/tail_probe.py): lane pixels ~1.6-2.4k clocks per pre-pass
+// step while whole-wave pixels take ~150-200 (bf_trace); group pixels ~0.8-1.5k
+constexpr float kDfsStep = 1900.0f, kDfsUse = 0.7f, kCoopStep = 180.0f;
+constexpr float kGroupStep = 850.0f, kGroupUse = 1.0f;
 
 // one thread: offsets, highest bucket first; hist[512] = items in buckets above the chosen split
 // (rendered by whole waves), hist[513] = their claim counter, hist[514] = items above `prio_bucket`
@@ -273,9 +285,9 @@ __global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, 
         // the largest lane pixel: the top of bucket b (or of the highest non-empty one)
         const int top = b < 0 ? -1 : top_of[b];
         const double maxc = top < 0 ? 0.0 : ldexp((double)(9 + (top & 7)) / 8.0, top >> 3) * m.spp_ratio;
-        const double lanes = (double)(m.grid_waves - wc) * 64.0;
-        const double t_dfs = fmax(maxc * kDfsStep, (total - coop_work) * m.spp_ratio * kDfsStep / (lanes * kDfsUse));
-        const double t_coop = wc ? coop_work * m.spp_ratio * kCoopStep / wc : 0.0;
+        const double lanes = (double)(m.grid_waves - wc) * m.lanes_per_wave;
+        const double t_dfs = fmax(maxc * m.dfs_step, (total - coop_work) * m.spp_ratio * m.dfs_step / (lanes * m.dfs_use));
+        const double t_coop = wc ? coop_work * m.spp_ratio * m.coop_step / wc : 0.0;
         const double t = fmax(t_dfs, t_coop);
         if (t < best_t) best_t = t, best_b = b, best_w = wc;
       }
@@ -283,6 +295,9 @@ __global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, 
   }
   uint32_t coop = 0;
   for (int k = 255; k > best_b; k--) coop += hist[k];
+  if (m.debug)
+    printf("[lpt_scan] ratio %f grid_waves %d dfs %f use %f coop %f lpw %d total %f best_b %d best_w %d\n", m.spp_ratio,
+           m.grid_waves, m.dfs_step, m.dfs_use, m.coop_step, m.lanes_per_wave, total, best_b, best_w);
   hist[512] = best_w > 0 ? coop : 0;
   hist[513] = 0;
   hist[514] = heavy;
@@ -733,7 +748,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
-                           4096,                                                             // [12] LPT buckets
+                           kLptHistBytes,                                                    // [12] LPT buckets
                            wide.size() * sizeof(uint4)};                                     // [13] treelets
   for (int k = 0; k < 14; k++) {
     off[k] = total;
@@ -862,7 +877,7 @@ extern "C" void rt_scene_release(rt_device_scene *d);
 // Buffers of the persistent general path: work counter, longest-first cost / order / buckets.
 static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const size_t npix = (size_t)s->camera.width * s->camera.height;
-  const size_t sizes[4] = {256, npix * sizeof(uint32_t), npix * sizeof(int32_t), 4096};
+  const size_t sizes[4] = {256, npix * sizeof(uint32_t), npix * sizeof(int32_t), kLptHistBytes};
   size_t off[4], total = 0;
   for (int k = 0; k < 4; k++) {
     off[k] = total;
@@ -1053,7 +1068,7 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       P.S.cam.spp = d->lpt_spp;
       P.cost_out = d->lpt_cost;
       if (launch_book1(d, P, d_out, st, true) != 0) return -1;
-      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 4096, st));
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
       unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);  // after the 516 counters
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
@@ -1061,7 +1076,12 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       const int coop_bucket = d->coop_steps < 0 ? -1 : (thr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)thr) : 255);
       LptModel model;
       model.spp_ratio = (float)V.S.cam.spp / (float)d->lpt_spp;
-      model.grid_waves = d->b1_grid * (b1::kBlock / 64);
+      model.grid_waves = (use_group ? d->g_grid : d->b1_grid) * (b1::kBlock / 64);
+      model.dfs_step = use_group ? kGroupStep : kDfsStep;
+      model.dfs_use = use_group ? kGroupUse : kDfsUse;
+      model.coop_step = kCoopStep;
+      model.lanes_per_wave = use_group ? 64 / grp::kG : 64;
+      model.debug = env_flag("RT_DEBUG", false) ? 1 : 0;
       const int64_t pthr = (int64_t)d->prio_steps * d->lpt_spp;
       const int prio_bucket = d->prio_steps > 0 && pthr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)pthr) : 256;
       hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, coop_bucket,
@@ -1080,24 +1100,13 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
         fprintf(stderr, "[rtc] lpt: %lld items, %u cooperative on %u waves (RT_COOP_STEPS %d, RT_COOP_WAVES %d; <0: "
                 "model), %u at raised priority\n", (long long)npix, nc, nw, d->coop_steps, d->coop_waves, nh);
       }
-      if (d->coop_waves != 0 && d->wave_stream && !use_group) {
+      if (d->coop_waves != 0 && d->wave_stream) {
         V.n_coop = d->lpt_hist + 512;
         V.coop_counter = (int32_t *)(d->lpt_hist + 513);
         V.coop_waves_dev = d->lpt_hist + 515;
       }
     }
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
-    if (use_group) {  // eight lanes per pixel (rt_group.h)
-      HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
-      const dim3 gg((unsigned)d->g_grid), gb(grp::kBlock);
-      if (d->book1_lds)
-        hipLaunchKernelGGL((rt_book1_group_kernel<true>), gg, gb, d->g_lds_bytes, st, V, d_out);
-      else
-        hipLaunchKernelGGL((rt_book1_group_kernel<false>), gg, gb, d->g_lds_bytes, st, V, d_out);
-      HIP_OK(hipGetLastError());
-      if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
-      return 0;
-    }
     const bool split = V.n_coop != nullptr;
     if (split) {  // whole-wave items: a concurrent kernel on the second stream (rt_book1.h: render_wave_items)
       HIP_OK(hipEventRecord(d->ev_fork, st));
@@ -1110,7 +1119,17 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
         hipLaunchKernelGGL((rt_book1_wave_kernel<false>), gw, blk, d->b1_lds_bytes, d->wave_stream, V, d_out);
       HIP_OK(hipGetLastError());
     }
-    if (launch_book1(d, V, d_out, st) != 0) return -1;
+    if (use_group) {  // eight lanes per pixel (rt_group.h)
+      HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+      const dim3 gg((unsigned)d->g_grid), gb(grp::kBlock);
+      if (d->book1_lds)
+        hipLaunchKernelGGL((rt_book1_group_kernel<true>), gg, gb, d->g_lds_bytes, st, V, d_out);
+      else
+        hipLaunchKernelGGL((rt_book1_group_kernel<false>), gg, gb, d->g_lds_bytes, st, V, d_out);
+      HIP_OK(hipGetLastError());
+    } else if (launch_book1(d, V, d_out, st) != 0) {
+      return -1;
+    }
     if (split) {
       HIP_OK(hipEventRecord(d->ev_join, d->wave_stream));
       HIP_OK(hipStreamWaitEvent(st, d->ev_join, 0));
@@ -1138,13 +1157,18 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
         hipLaunchKernelGGL(rt_general_kernel<kFeatAll>, gg, gb, 0, st, P, d_out);
       else
         hipLaunchKernelGGL(rt_general_kernel<kFeatBook1>, gg, gb, 0, st, P, d_out);
-      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, 4096, st));
+      HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
       unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
       LptModel model;
       model.spp_ratio = 1.0f;
       model.grid_waves = d->gen_grid * (gen::kBlock / 64);
+      model.dfs_step = kDfsStep;
+      model.dfs_use = kDfsUse;
+      model.coop_step = kCoopStep;
+      model.lanes_per_wave = 64;
+      model.debug = 0;
       hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, 255, 0, 256, model);
       hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
       HIP_OK(hipGetLastError());
