@@ -70,6 +70,7 @@ struct Book1View {
   uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end}, wall_clock64 low bits
   const uint4 *wide;         // group trace (rt_group.h): 8-entry treelets over the preorder items
   int32_t n_wide;            // 0: group kernel unavailable for this scene
+  const uint16_t *anc;       // group trace: [item][16] ancestor item positions of each leaf (0xffff: none)
 };
 
 // ---------------------------------------------------------------- wave helpers

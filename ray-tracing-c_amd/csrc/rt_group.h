@@ -28,69 +28,61 @@ namespace rt {
 namespace grp {
 
 constexpr int kG = 8;                  // lanes per pixel
+constexpr uint32_t kGMask = (1u << kG) - 1u;
 constexpr int kBlock = b1::kBlock;     // 256 threads: 32 groups
 constexpr int kGroups = kBlock / kG;
 constexpr int kStack = 32;             // LDS stack entries per group (overflow: exact scan)
 constexpr uint32_t kEmpty = 0xffffffffu;
-// wide entry (uint4): x = item position (kEmpty: none), y = child treelet (internal entries),
-//                     z = inter0 | inter1 << 16, w = inter2 | n_inter << 16
-
-RT_D float sphere_root_g(float4 s, const b1::CoopRay &C, float tmin) { return b1::coop_sphere_root(s, C, tmin); }
+// treelet slot k (uint4): x = entry k's item position (kEmpty: none), y = its child treelet (internal
+// entries), z = its chain (bit c: opened internal node c of the treelet lies between the treelet's
+// root and the entry) | leaf << 8, w = the item position of opened internal node k (kEmpty: none).
+constexpr int kMaxAnc = 16;  // ancestors per leaf in the verification table (host-checked)
 
 // One ray of this lane's group; returns false when the rule cannot decide (the caller scans).
-// out: t_max, and the winning leaf's item position (-1: a miss).
-RT_D bool group_trace(const b1::Book1View &V, const float4 *items, uint2 *stk, const b1::CoopRay &C, float tmin,
+// out: t_max, and the winning leaf's item position (-1: a miss).  Lane k of the group tests the
+// treelet's internal node k and entry k: an entry counts when its chain's internals all pass.  The
+// winner's ancestors are then checked against its root (E < r*) from the per-leaf table V.anc.
+RT_D bool group_trace(const b1::Book1View &V, const float4 *items, uint32_t *stk, const b1::CoopRay &C, float tmin,
                       float &out_t, int &out_pos) {
   const int lane = __lane_id();
   const int g = lane & (kG - 1), base = lane & ~(kG - 1);
-  float best = __builtin_inff(), best_e = -__builtin_inff();
+  float best = __builtin_inff();
   int bpos = 0x7fffffff;
   bool nan = false, overflow = false;
-  uint32_t cur = 0;                  // treelet 0: the root list's items
-  float cur_e = -__builtin_inff();  // max E over the treelet's tested ancestors
+  uint32_t cur = 0;  // treelet 0: the root list's items
   int sp = 0;
   bool active = true;
   while (__ballot(active) != 0) {
-    bool push = false;
-    float push_e = 0.0f;
+    bool push = false, ipass = true;
     uint32_t child = 0;
+    uint4 e = make_uint4(kEmpty, 0u, 0u, kEmpty);
     if (active) {
-      const uint4 e = V.wide[cur * kG + g];
-      if (e.x != kEmpty) {
-        float emax = cur_e;
-        bool ok = true;
-        const uint32_t n_inter = e.w >> 16;
-        const uint32_t inter[3] = {e.z & 0xffffu, e.z >> 16, e.w & 0xffffu};
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-          if ((uint32_t)q < n_inter) {
-            const uint32_t it = inter[q];
-            float be, bx;
-            b1::box_interval(items[2 * it], items[2 * it + 1], C, tmin, be, bx);
-            ok = ok && fminf(__builtin_inff(), bx) > be;
-            emax = fmaxf(emax, be);
-          }
-        }
-        if (ok) {
-          const float4 q0 = items[2 * e.x], q1 = items[2 * e.x + 1];
-          if (__float_as_uint(q1.w) & b1::kLeaf9) {
-            const float r = sphere_root_g(q0, C, tmin);
-            nan |= r != r;
-            if (r > tmin && (r < best || (r == best && (int)e.x < bpos))) best = r, bpos = (int)e.x, best_e = emax;
-          } else {
-            float be, bx;
-            b1::box_interval(q0, q1, C, tmin, be, bx);
-            if (fminf(__builtin_inff(), bx) > be) push = true, push_e = fmaxf(emax, be), child = e.y;
-          }
-        }
+      e = V.wide[cur * kG + g];
+      if (e.w != kEmpty) {
+        float be, bx;
+        b1::box_interval(items[2 * e.w], items[2 * e.w + 1], C, tmin, be, bx);
+        ipass = fminf(__builtin_inff(), bx) > be;
+      }
+    }
+    const uint32_t fail = (uint32_t)(__ballot(!ipass) >> base) & kGMask;  // the group's failing internals
+    if (active && e.x != kEmpty && (e.z & fail & 0xffu) == 0u) {
+      const float4 q0 = items[2 * e.x];
+      if (e.z & 0x100u) {
+        const float r = b1::coop_sphere_root(q0, C, tmin);
+        nan |= r != r;
+        if (r > tmin && (r < best || (r == best && (int)e.x < bpos))) best = r, bpos = (int)e.x;
+      } else {
+        float be, bx;
+        b1::box_interval(q0, items[2 * e.x + 1], C, tmin, be, bx);
+        if (fminf(__builtin_inff(), bx) > be) push = true, child = e.y;
       }
     }
     // push the group's passing internal entries (a ballot slice per group), then pop one
-    const uint32_t m = (uint32_t)(__ballot(push) >> base) & 0xffu;
+    const uint32_t m = (uint32_t)(__ballot(push) >> base) & kGMask;
     if (push) {
       const int at = sp + __popc(m & ((1u << g) - 1u));
       if (at < kStack)
-        stk[at] = make_uint2(child, __float_as_uint(push_e));
+        stk[at] = child;
       else
         overflow = true;
     }
@@ -104,28 +96,36 @@ RT_D bool group_trace(const b1::Book1View &V, const float4 *items, uint2 *stk, c
         active = false;
       } else {
         sp--;
-        const uint2 t = stk[sp];
-        cur = t.x;
-        cur_e = __uint_as_float(t.y);
+        cur = stk[sp];
       }
     }
     __builtin_amdgcn_wave_barrier();  // the next iteration's pushes may overwrite the popped slot
   }
-  // group reduction over (root, preorder position); carry the winner's ancestor E
+  // group reduction over (root, preorder position)
 #pragma unroll
   for (int off = kG / 2; off >= 1; off >>= 1) {
-    const float ob = __shfl_xor(best, off), oe = __shfl_xor(best_e, off);
+    const float ob = __shfl_xor(best, off);
     const int op = __shfl_xor(bpos, off);
-    if (ob < best || (ob == best && op < bpos)) best = ob, bpos = op, best_e = oe;
+    if (ob < best || (ob == best && op < bpos)) best = ob, bpos = op;
   }
-  const uint64_t bad = __ballot(nan || overflow);
-  if ((bad >> base) & 0xffu) return false;
+  bool bad = nan || overflow;
+  if (bpos != 0x7fffffff) {  // the winner's ancestors (all passed t_max-free): E < r* at each
+#pragma unroll
+    for (int q = 0; q < kMaxAnc; q += kG) {
+      const uint32_t a = V.anc[(uint32_t)bpos * kMaxAnc + q + g];
+      if (a != 0xffffu) {
+        float be, bx;
+        b1::box_interval(items[2 * a], items[2 * a + 1], C, tmin, be, bx);
+        bad |= !(fminf(best, bx) > be);
+      }
+    }
+  }
+  if ((__ballot(bad) >> base) & kGMask) return false;
   if (bpos == 0x7fffffff) {
     out_t = __builtin_inff();
     out_pos = -1;
     return true;
   }
-  if (!(best_e < best)) return false;  // an ancestor box might cull s*: decide by the scan
   out_t = best;
   out_pos = bpos;
   return true;
@@ -143,14 +143,14 @@ __device__ void render_groups(const b1::Book1View &V, uint8_t *__restrict__ out,
     return;
   const int64_t work_offset = V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   float4 *items = (float4 *)lds;
-  uint2 *stacks = (uint2 *)(items + (kLds ? 2 * V.n_items9_alloc : 0));
+  uint32_t *stacks = (uint32_t *)(items + (kLds ? 2 * V.n_items9_alloc : 0));
   if (kLds) {
     for (int q = tid; q < 2 * V.n_items9_alloc; q += kBlock) items[q] = V.items9_g[q];
     __syncthreads();
   } else {
     items = (float4 *)V.items9_g;
   }
-  uint2 *stk = stacks + (tid / kG) * kStack;
+  uint32_t *stk = stacks + (tid / kG) * kStack;
   const int lane = __lane_id();
   const int g = lane & (kG - 1), base = lane & ~(kG - 1);
   const int spill_lane = (int)(blockIdx.x * kBlock + tid) / kG;  // one record spill column per group

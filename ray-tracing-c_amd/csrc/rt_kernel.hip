@@ -590,9 +590,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     else
       h.w = bits_as_float(bf_item[n]);
   }
-  // group trace treelets (rt_group.h): greedy 8-entry treelets over the preorder items, each entry
-  // with up to 3 intermediate nodes between it and the treelet's (already tested) root
+  // group trace treelets (rt_group.h): greedy treelets of <= 8 entries over the preorder items, each
+  // entry with <= 3 opened internal nodes between it and the treelet's (already tested) root; and the
+  // per-leaf ancestor table for the winner's check
   std::vector<uint4> wide;
+  std::vector<uint16_t> anc;
   {
     const int n_items = (int)(items9.size() / 2) - 1;  // without the pad item
     auto is_leaf = [&](int p) {
@@ -614,37 +616,37 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
       return n;
     };
     struct E {
-      int item, n_inter, inter[3];
+      int item, n_chain;
+      uint32_t need;
     };
     bool ok = n_items > 0 && n_items < 0xffff;
     std::function<int(const std::vector<int> &)> make = [&](const std::vector<int> &level1) -> int {
       if (!ok || level1.size() > (size_t)grp::kG) return ok = false, -1;
       std::vector<E> es;
-      for (int c : level1) es.push_back({c, 0, {0, 0, 0}});
+      std::vector<int> internals;
+      for (int c : level1) es.push_back({c, 0, 0u});
       for (;;) {  // open the internal entry with the largest subtree while the treelet has room
         int pick = -1;
         for (int k = 0; k < (int)es.size(); k++) {
           int kc[2];
-          if (is_leaf(es[k].item) || es[k].n_inter >= 3 || (int)es.size() + kids(es[k].item, kc) - 1 > grp::kG)
+          if (is_leaf(es[k].item) || es[k].n_chain >= 3 || (int)es.size() + kids(es[k].item, kc) - 1 > grp::kG)
             continue;
           if (pick < 0 || size_of(es[k].item) > size_of(es[pick].item)) pick = k;
         }
-        if (pick < 0) break;
+        if (pick < 0 || (int)internals.size() >= grp::kG) break;
         const E old = es[pick];
         int kc[2];
         const int nc = kids(old.item, kc);
+        const uint32_t bit = 1u << internals.size();
+        internals.push_back(old.item);
         std::vector<E> repl;
-        for (int c = 0; c < nc; c++) {
-          E e = old;
-          e.item = kc[c];
-          e.inter[e.n_inter++] = old.item;
-          repl.push_back(e);
-        }
+        for (int c = 0; c < nc; c++) repl.push_back({kc[c], old.n_chain + 1, old.need | bit});
         es.erase(es.begin() + pick);
         es.insert(es.begin() + pick, repl.begin(), repl.end());
       }
       const int id = (int)(wide.size() / grp::kG);
-      for (int k = 0; k < grp::kG; k++) wide.push_back(make_uint4(grp::kEmpty, 0u, 0u, 0u));
+      for (int k = 0; k < grp::kG; k++)
+        wide.push_back(make_uint4(grp::kEmpty, 0u, 0u, k < (int)internals.size() ? (uint32_t)internals[k] : grp::kEmpty));
       for (int k = 0; k < (int)es.size(); k++) {
         const E &e = es[k];
         uint32_t child = 0;
@@ -655,15 +657,34 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
           if (c < 0) return -1;
           child = (uint32_t)c;
         }
-        wide[(size_t)id * grp::kG + k] =
-            make_uint4((uint32_t)e.item, child, (uint32_t)e.inter[0] | (uint32_t)e.inter[1] << 16,
-                       (uint32_t)e.inter[2] | (uint32_t)e.n_inter << 16);
+        uint4 &w = wide[(size_t)id * grp::kG + k];
+        w.x = (uint32_t)e.item, w.y = child, w.z = e.need | (is_leaf(e.item) ? 0x100u : 0u);
       }
       return id;
     };
     std::vector<int> tops;
     for (int p = 0; p < n_items; p += size_of(p)) tops.push_back(p);
     if (make(tops) != 0 || !ok) wide.clear();
+    // ancestors of every leaf, root first
+    if (!wide.empty()) {
+      anc.assign((size_t)(n_items + 1) * grp::kMaxAnc, 0xffffu);
+      std::vector<int> path;
+      std::function<void(int)> walk = [&](int p) {
+        if (!ok) return;
+        if (is_leaf(p)) {
+          if ((int)path.size() > grp::kMaxAnc) return void(ok = false);
+          for (size_t q = 0; q < path.size(); q++) anc[(size_t)p * grp::kMaxAnc + q] = (uint16_t)path[q];
+          return;
+        }
+        path.push_back(p);
+        int kc[2];
+        const int nc = kids(p, kc);
+        for (int c = 0; c < nc; c++) walk(kc[c]);
+        path.pop_back();
+      };
+      for (int t : tops) walk(t);
+      if (!ok) wide.clear(), anc.clear();
+    }
   }
   std::vector<float4> sph(s->n_spheres);
   for (int k = 0; k < s->n_spheres; k++)
@@ -740,17 +761,17 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth / 4) * spill_lanes * sizeof(uint64_t);  // Record chunks
 
-  size_t off[14], total = 0;
+  size_t off[15], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[14] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+  const size_t sizes[15] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
                            roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
                            nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t),
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
                            kLptHistBytes,                                                    // [12] LPT buckets
-                           wide.size() * sizeof(uint4)};                                     // [13] treelets
-  for (int k = 0; k < 14; k++) {
+                           wide.size() * sizeof(uint4), anc.size() * sizeof(uint16_t)};      // [13] [14] group
+  for (int k = 0; k < 15; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -765,6 +786,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   HIP_OK(hipMemcpy(b + off[8], roots7.data(), sizes[8], hipMemcpyHostToDevice));
   if (sizes[9]) HIP_OK(hipMemcpy(b + off[9], items9.data(), sizes[9], hipMemcpyHostToDevice));
   if (sizes[13]) HIP_OK(hipMemcpy(b + off[13], wide.data(), sizes[13], hipMemcpyHostToDevice));
+  if (sizes[14]) HIP_OK(hipMemcpy(b + off[14], anc.data(), sizes[14], hipMemcpyHostToDevice));
   d->b1_arena = arena;
   b1::Book1View &V = d->b1view;
   V.S = d->view;
@@ -782,6 +804,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   V.items9_g = (const float4 *)(b + off[9]);
   V.wide = (const uint4 *)(b + off[13]);
   V.n_wide = (int32_t)(wide.size() / grp::kG);
+  V.anc = (const uint16_t *)(b + off[14]);
   {  // the group kernel (rt_group.h), for frames with few pixels per lane
     const char *em = getenv("RT_MODE");
     d->group_mode = (em && !strcmp(em, "lane")) ? 0 : (em && !strcmp(em, "group")) ? 1 : 2;
@@ -789,7 +812,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     if (d->group_mode != 0) {
       const bool lds = d->book1_lds;
       d->g_lds_bytes = align_up((lds ? items9.size() * sizeof(float4) : 0) +
-                                    (size_t)grp::kGroups * grp::kStack * sizeof(uint2), 16);
+                                    (size_t)grp::kGroups * grp::kStack * sizeof(uint32_t), 16);
       int per = 0;
       HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
           &per, lds ? (const void *)rt_book1_group_kernel<true> : (const void *)rt_book1_group_kernel<false>,
