@@ -232,11 +232,10 @@ __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist, uns
   }
 }
 
-// Cost model of one launch for the split between whole-wave pixels (render_pixel_coop) and lane
-// pixels, in clocks (measured on the headline frame): a lane pixel advances one
-// traversal step per kDfsStep clocks, the lanes together at kDfsUse of that rate; a whole-wave
-// pixel costs kCoopStep clocks per step.  The frame ends when both the slowest lane pixel and the
-// whole-wave queue are done.
+// Cost model of one launch for the split between whole-wave pixels (render_pixel_coop) and lane (or
+// group) pixels, in clocks per pre-pass step (measured on the headline frame): the
+// frame ends when the slowest lane pixel's chain (lat_step), the lanes' aggregate work (thr_step per
+// lane), the whole-wave queue and the heaviest whole-wave pixel's chain (coop_step) are all done.
 // LPT scratch: 256 bucket counts, 256 running offsets, 4 split counters (u32 [512..515]), then from
 // u32 544 the 256 per-bucket step sums (u64): 2176 + 2048 bytes
 constexpr size_t kLptHistBytes = 8192;
@@ -244,16 +243,16 @@ constexpr size_t kLptHistBytes = 8192;
 struct LptModel {
   float spp_ratio;  // frame spp / pre-pass spp (costs are pre-pass steps)
   int grid_waves;
-  float dfs_step;   // clocks per step of a lane (or group) pixel under load
-  float dfs_use;    // the lanes' (groups') aggregate rate, as a fraction of dfs_step per lane (group)
-  float coop_step;  // clocks per step of a whole-wave pixel
+  float lat_step;   // clocks per step of the slowest lane (group) pixels under load: their chain
+  float thr_step;   // clocks per step per lane (group) of all lanes' (groups') aggregate rate
+  float coop_step;  // clocks per step of a whole-wave pixel (its chain, and its wave's rate)
   int lanes_per_wave;  // pixels in flight per non-cooperative wave: 64 lanes, or 8 groups
   int debug;           // RT_DEBUG: print the model's inputs and choice
 };
-// measured on the headline frame (scripts/tail_probe.py): lane pixels ~1.6-2.4k clocks per pre-pass
-// step while whole-wave pixels take ~150-200 (bf_trace); group pixels ~0.8-1.5k
-constexpr float kDfsStep = 1900.0f, kDfsUse = 0.7f, kCoopStep = 180.0f;
-constexpr float kGroupStep = 850.0f, kGroupUse = 1.0f;
+// clocks per pre-pass step, fitted to frame times on one MI355X (scripts/tail_probe.py measures the
+// per-pixel rates: lane pixels ~1.6-4k by load, group ~0.6-1.1k, whole-wave ~120-180)
+constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kGroupLat = 850.0f, kGroupThr = 850.0f;
+constexpr float kCoopStep = 180.0f, kCoopStepLane = 250.0f;
 
 // one thread: offsets, highest bucket first; hist[512] = items in buckets above the chosen split
 // (rendered by whole waves), hist[513] = their claim counter, hist[514] = items above `prio_bucket`
@@ -274,6 +273,8 @@ __global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, 
     // highest non-empty bucket at or below each bucket (the largest lane pixel of a split)
     int16_t top_of[256];
     for (int k = 0, t = -1; k < 256; k++) top_of[k] = (int16_t)(t = hist[k] ? k : t);
+    const double top_all = top_of[255] < 0 ? 0.0
+                                           : ldexp((double)(9 + (top_of[255] & 7)) / 8.0, top_of[255] >> 3) * m.spp_ratio;
     double best_t = 1e300;
     for (int wc = 0; wc <= m.grid_waves / 2; wc = wc ? 2 * wc : 128) {
       if (coop_waves >= 0 && wc != coop_waves) continue;
@@ -286,8 +287,9 @@ __global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, 
         const int top = b < 0 ? -1 : top_of[b];
         const double maxc = top < 0 ? 0.0 : ldexp((double)(9 + (top & 7)) / 8.0, top >> 3) * m.spp_ratio;
         const double lanes = (double)(m.grid_waves - wc) * m.lanes_per_wave;
-        const double t_dfs = fmax(maxc * m.dfs_step, (total - coop_work) * m.spp_ratio * m.dfs_step / (lanes * m.dfs_use));
-        const double t_coop = wc ? coop_work * m.spp_ratio * m.coop_step / wc : 0.0;
+        const double t_dfs = fmax(maxc * m.lat_step, (total - coop_work) * m.spp_ratio * m.thr_step / lanes);
+        // whole waves: their queue, and the heaviest pixel's own chain
+        const double t_coop = wc ? fmax(coop_work * m.spp_ratio * m.coop_step / wc, top_all * m.coop_step) : 0.0;
         const double t = fmax(t_dfs, t_coop);
         if (t < best_t) best_t = t, best_b = b, best_w = wc;
       }
@@ -296,8 +298,8 @@ __global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, 
   uint32_t coop = 0;
   for (int k = 255; k > best_b; k--) coop += hist[k];
   if (m.debug)
-    printf("[lpt_scan] ratio %f grid_waves %d dfs %f use %f coop %f lpw %d total %f best_b %d best_w %d\n", m.spp_ratio,
-           m.grid_waves, m.dfs_step, m.dfs_use, m.coop_step, m.lanes_per_wave, total, best_b, best_w);
+    printf("[lpt_scan] ratio %f grid_waves %d lat %f thr %f coop %f lpw %d total %f best_b %d best_w %d\n", m.spp_ratio,
+           m.grid_waves, m.lat_step, m.thr_step, m.coop_step, m.lanes_per_wave, total, best_b, best_w);
   hist[512] = best_w > 0 ? coop : 0;
   hist[513] = 0;
   hist[514] = heavy;
@@ -1100,11 +1102,13 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       LptModel model;
       model.spp_ratio = (float)V.S.cam.spp / (float)d->lpt_spp;
       model.grid_waves = (use_group ? d->g_grid : d->b1_grid) * (b1::kBlock / 64);
-      model.dfs_step = use_group ? kGroupStep : kDfsStep;
-      model.dfs_use = use_group ? kGroupUse : kDfsUse;
-      model.coop_step = kCoopStep;
+      model.lat_step = use_group ? kGroupLat : kLaneLat;
+      model.thr_step = use_group ? kGroupThr : kLaneThr;
+      model.coop_step = use_group ? kCoopStep : kCoopStepLane;
       model.lanes_per_wave = use_group ? 64 / grp::kG : 64;
       model.debug = env_flag("RT_DEBUG", false) ? 1 : 0;
+      if (const char *em = getenv(use_group ? "RT_MODEL_GROUP" : "RT_MODEL_LANE"))  // "lat,thr,coop" (tuning)
+        sscanf(em, "%f,%f,%f", &model.lat_step, &model.thr_step, &model.coop_step);
       const int64_t pthr = (int64_t)d->prio_steps * d->lpt_spp;
       const int prio_bucket = d->prio_steps > 0 && pthr < (int64_t)UINT32_MAX ? (int)host_lpt_bucket((uint32_t)pthr) : 256;
       hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, coop_bucket,
@@ -1187,8 +1191,8 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       LptModel model;
       model.spp_ratio = 1.0f;
       model.grid_waves = d->gen_grid * (gen::kBlock / 64);
-      model.dfs_step = kDfsStep;
-      model.dfs_use = kDfsUse;
+      model.lat_step = kLaneLat;
+      model.thr_step = kLaneThr;
       model.coop_step = kCoopStep;
       model.lanes_per_wave = 64;
       model.debug = 0;
