@@ -36,6 +36,33 @@ struct FastMat {   // 32 B: material resolved to what the Book-1 path needs
   int32_t pad[3];
 };
 
+// Split render (stream split, render_batched kMode 2).  A pixel's samples share one pcg32 stream:
+// sample s starts at stream offset o_s and draws D(o_s), so o_{s+1} = o_s + D(o_s), and a sample's
+// colour and draw count are functions of its start offset alone.  A split pixel's stream [0, len)
+// is cut into K segments at offsets B_k.  Segment 0 is the pixel's head chain (samples in order from
+// offset 0, accumulated like an unsplit pixel).  Segment k > 0 runs chains from each offset of the
+// window [B_k, B_k + w) in turn, sample after sample until the segment's end, storing each sample's
+// colour and draw count at its offset; a chain stops at an offset another chain already claimed, so
+// the window's chains coalesce.  split_walk_kernel then follows the true chain through the records
+// and adds the sample colours in sample order -- the reference's summation order, so the pixel is
+// bit-identical.  An offset the true chain needs but no chain evaluated (a draw count larger than
+// the window, or a stream longer than len) continues as a head chain in a fix-up round.
+// The records are allocated past the estimate (len > len_run): a stream longer than the chains of
+// the first round covered is split again from the walk's exact position (split_replan_kernel).
+struct SplitPx {            // 48 B per work item of a split launch
+  float acc[3];             // head chain: colour sum of samples [0, s)
+  uint32_t o, s;            // head chain: next sample's start offset and index (s == spp: written)
+  uint32_t stop_at;         // head chain stops at this offset (segment 0's end), or kNoStop / kNoCoalesce
+  uint32_t base, len;       // records of offsets [segment 0's end, len) at sp_claim / sp_rec [base + o]
+  uint32_t len_run;         // offsets below this are covered by segment chains already
+  uint32_t w;               // window: chains per segment
+  float cps;                // pre-pass traversal steps per sample
+  uint32_t rec_lo;          // segment 0's end: records (and claims) exist for offsets >= rec_lo
+};
+constexpr uint32_t kNoStop = 0xffffffffu;      // stop at a claimed offset only (fix-up rounds)
+constexpr uint32_t kNoCoalesce = 0xfffffffeu;  // never stop before spp samples (unsplit pixels, last round)
+constexpr uint32_t kSpecBit = 0x80000000u;     // sp_items[].x: segment item (else head item)
+
 struct Book1View {
   DScene S;                  // full scene (global memory): sphere aux data, camera
   const float4 *nodes_g;     // 2 float4 per node: (lo.x hi.x lo.y hi.y), (lo.z hi.z left right bits)
@@ -71,6 +98,15 @@ struct Book1View {
   const uint4 *wide;         // group trace (rt_group.h): 8-entry treelets over the preorder items
   int32_t n_wide;            // 0: group kernel unavailable for this scene
   const uint16_t *anc;       // group trace: [item][16] ancestor item positions of each leaf (0xffff: none)
+  uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
+  SplitPx *sp_px;            // split render (kMode 2): per work item state
+  uint32_t *sp_claim;        //   per stream offset: 0 free, 1 claimed (its record is written)
+  float4 *sp_rec;            //   per stream offset: sample colour, draw count (bits in .w)
+  const uint4 *sp_items;     //   chains: {pix | kSpecBit, B, E, w} segment, or {pix, -, -, -} head
+  const uint32_t *sp_n_items;
+  const uint4 *sp_items2;    //   then these (segment chains of re-split pixels, fix-up rounds), or null
+  const uint32_t *sp_n_items2;
+  uint32_t sp_cap2;          //   (its capacity: the count may run past it)
 };
 
 // ---------------------------------------------------------------- wave helpers
@@ -1214,7 +1250,8 @@ constexpr int kSteps = 4;
 
 // kStats: diagnostic build only (RT_BOOK1_STATS=1) — per-lane counters of where wave iterations go,
 // accumulated into V.stats with one atomic per lane at exit; never used for timing.
-template <bool kLds, bool kStats = false, int kStep = 5>
+// kMode: 0 frame, 1 cost pre-pass (also counts draws per item), 2 split render (SplitPx above).
+template <bool kLds, bool kStats = false, int kStep = 5, int kMode = 0>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
   // the last workgroups of the grid leave their CU slots to the whole-wave kernel (render_wave_items)
@@ -1279,6 +1316,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   Pcg32 g;
   g.state = 0;
   g.inc = 0;
+  g.n = 0;
+  // split render: the chain's next sample offset and its end (the pixel's record range is re-read
+  // from sp_px at sample boundaries: fewer live registers in the traversal loop)
+  uint32_t so = 0, send = 0;
+  bool spec = false;
   f3 acc = mk(0, 0, 0);
   Record R;
   R.r0 = R.r1 = 0;
@@ -1295,7 +1337,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   // the heaviest items (the first *n_coop of the order) are rendered by whole waves in the concurrent
   // rt_book1_wave_kernel (render_wave_items); the lanes' own items start after them
   const int64_t work_offset = V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
-  const int64_t total_own = total - work_offset;
+  const int64_t n_items1 = kMode == 2 ? (int64_t)*V.sp_n_items : 0;
+  const int64_t total_own =
+      kMode == 2 ? n_items1 + (V.sp_items2 ? (int64_t)min(*V.sp_n_items2, V.sp_cap2) : 0) : total - work_offset;
   const int64_t n_heavy = (V.order && V.n_heavy) ? (int64_t)*V.n_heavy : 0;
   bool heavy = false;  // this lane's pixel is among the n_heavy longest
   bool prio = false;
@@ -1413,12 +1457,23 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         depth--;
         path_done = depth <= 0;  // the next call would return 0 at depth 0 (src/raytracing.c:40)
       }
-      if (path_done) {
+      if (kMode == 2 && path_done) {  // split render: the chain check below decides what follows
+        const f3 col = rec_fold(V, R, tail, glane);
+        if (spec) {
+          V.sp_rec[V.sp_px[pix].base + so] = make_float4(col.x, col.y, col.z, __uint_as_float(g.n - so));
+        } else {
+          acc = add(acc, col);
+          s++;
+        }
+        so = g.n;
+        need_sample = true;
+      } else if (path_done) {
         acc = add(acc, rec_fold(V, R, tail, glane));
         s++;
         if (s == spp) {  // quantize (src/raytracing.c:127-131)
           write_pixel(out + pix * 3, acc, spp);
           if (V.cost_out) V.cost_out[pix] = px_steps;
+          if (kMode == 1) V.draw_out[pix] = g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kStats) {
             V.pixel_cost[2 * pix] = px_steps;
@@ -1443,19 +1498,58 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           mode = kExit;
           break;
         }
-        heavy = pix + work_offset < n_heavy;
-        if (V.order) pix = V.order[pix + work_offset];  // longest work items first
-        else if (V.reverse) pix = total - 1 - pix;
+        uint4 it = make_uint4(0u, 0u, 0u, 0u);
+        if (kMode == 2) {  // a chain of the split launch (its items are already in longest-first order)
+          it = pix < n_items1 ? V.sp_items[pix] : V.sp_items2[pix - n_items1];
+          spec = (it.x & kSpecBit) != 0u;
+          pix = (int64_t)(it.x & ~kSpecBit);
+        } else {
+          heavy = pix + work_offset < n_heavy;
+          if (V.order) pix = V.order[pix + work_offset];  // longest work items first
+          else if (V.reverse) pix = total - 1 - pix;
+        }
         const int jj = (int)(pix / W);
         i = (int)(pix - (int64_t)jj * W);
         j = V.row0 + jj * V.row_stride;
         g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
         acc = mk(0.0f, 0.0f, 0.0f);
         s = 0;
+        if (kMode == 2) {
+          const SplitPx &P = V.sp_px[pix];
+          if (spec) {  // a chain from offset it.y to the segment's end it.z
+            so = it.y, send = it.z;
+          } else {  // the head chain, from where the last round left it
+            acc = mk(P.acc[0], P.acc[1], P.acc[2]);
+            so = P.o, s = (int)P.s, send = P.stop_at;
+          }
+          g.skip(so);
+        }
         need_pixel = false;
         px_steps = 0;
         if (V.px_time) V.px_time[2 * pix] = (uint32_t)wall_clock64();
         if (kStats) px_t0 = (long long)wall_clock64();
+      }
+      if (kMode == 2) {  // the chain check at a sample boundary
+        const uint32_t sbase = V.sp_px[pix].base, slen = V.sp_px[pix].len, srec_lo = V.sp_px[pix].rec_lo;
+        if (!spec) {
+          if (s == spp) {  // the pixel's last sample: quantize (src/raytracing.c:127-131)
+            write_pixel(out + pix * 3, acc, spp);
+            V.sp_px[pix].s = (uint32_t)spp;
+            need_pixel = true;
+            continue;
+          }
+          // (records exist only past segment 0: sbase + o is a valid index for o >= segment 0's end)
+          if (so >= send || (send != kNoCoalesce && so >= srec_lo && so < slen && V.sp_claim[sbase + so] != 0u)) {
+            SplitPx &P = V.sp_px[pix];  // segment 0 done, or joined evaluated records: the walk goes on
+            P.acc[0] = acc.x, P.acc[1] = acc.y, P.acc[2] = acc.z;
+            P.o = so, P.s = (uint32_t)s;
+            need_pixel = true;
+            continue;
+          }
+        } else if (!(so < send && so < slen && atomicCAS(&V.sp_claim[sbase + so], 0u, 1u) == 0u)) {
+          need_pixel = true;  // a chain ends at its segment's end or at an offset another chain owns
+          continue;
+        }
       }
       // camera ray (src/raytracing.c:96-122)
       const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
@@ -1477,7 +1571,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       depth = max_depth;
       R.n = 0;
       need_sample = false;
-      if (depth <= 0) {  // Camera_ray_color returns 0 without tracing
+      if (kMode != 2 && depth <= 0) {  // Camera_ray_color returns 0 without tracing (host: split needs depth >= 1)
         acc = add(acc, mk(0.0f, 0.0f, 0.0f));
         s++;
         if (s == spp) {

@@ -56,9 +56,11 @@ RT_D f3 ray_at(f3 o, f3 d, float t) { return add(o, scale(d, t)); }
 // ------------------------------------------------------------------------------ pcg32
 struct Pcg32 {
   uint64_t state, inc;
+  uint32_t n;  // draws since seed(): the stream offset (split render, rt_book1.h); dead code elsewhere
   RT_D uint32_t next() {
     const uint64_t s = state;
     state = s * 6364136223846793005ULL + inc;
+    n++;
     const uint32_t x = (uint32_t)(((s >> 18u) ^ s) >> 27u);
     return __builtin_rotateright32(x, (uint32_t)(s >> 59u));
   }
@@ -68,6 +70,19 @@ struct Pcg32 {
     (void)next();
     state += initstate;
     (void)next();
+    n = 0;
+  }
+  // advance by k draws without generating them: the LCG's k-step map (a^k, c*(a^k-1)/(a-1)) by
+  // squaring, O(log k) 64-bit multiplies (pcg32_advance semantics)
+  RT_D void skip(uint32_t k) {
+    uint64_t am = 6364136223846793005ULL, ac = inc, mul = 1u, add = 0u;
+    for (uint32_t r = k; r != 0u; r >>= 1) {
+      if (r & 1u) mul *= am, add = add * am + ac;
+      ac = (am + 1u) * ac;
+      am *= am;
+    }
+    state = mul * state + add;
+    n += k;
   }
   RT_D float f32() { return (float)(next() >> 8) * 0x1p-24f; }  // == (float)(u>>8) / 2^24
   RT_D float between(float lo, float hi) { return lo + f32() * (hi - lo); }

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <mutex>
 #include <functional>
@@ -93,7 +94,98 @@ __global__ __launch_bounds__(b1::kBlock) void rt_book1_wave_kernel(b1::Book1View
 template <bool kLds, int kVer>
 __global__ __launch_bounds__(b1::kBlock) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  b1::render_batched<kLds, false, kVer>(V, out, lds);
+  b1::render_batched<kLds, false, kVer, 1>(V, out, lds);
+}
+
+// Split render (rt_book1.h: SplitPx): the chains of one round -- head chains and segment windows.
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_split_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  b1::render_batched<kLds, false, 9, 2>(V, out, lds);
+}
+
+// Split render: expand the host's entries (a head chain, or a segment's window {pix, B, E, w}) into
+// one chain per window start offset, in the entries' (longest-first) order.
+__global__ void split_expand_kernel(const uint4 *ent, const uint32_t *pre, uint32_t n, uint4 *items) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint4 x = ent[e];
+    const uint32_t w = x.w ? x.w : 1u, at = pre[e];
+    for (uint32_t q = 0; q < w; q++) items[at + q] = make_uint4(x.x, x.y + q, x.z, 1u);
+  }
+}
+
+// Split render, before a fix-up round: the chains for the pixels the walk left unfinished.  A pixel
+// whose stream ran past the offsets its segment chains covered (the pre-pass under-estimated it) is
+// split again from its exact position, with the stream length now estimated from its own samples;
+// any other continues as a head chain (it coalesces with the records at the next claimed offset).
+// The heads stay in the walk's list (sp_items); the new segment chains go to sp_items2 (one wave per
+// pixel writes them).  A reservation past `cap` is filled with empty chains (start past end).
+__global__ void split_replan_kernel(b1::Book1View V, const uint4 *heads, const uint32_t *n_heads, uint4 *items,
+                                    uint32_t *n_items, uint32_t cap, float cstar, float margin, int kmax, int last_round) {
+  const uint32_t n = *n_heads;
+  const uint32_t spp = (uint32_t)V.S.cam.spp;
+  const int lane = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / 64);
+  for (uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) / 64; k < n; k += waves) {
+    const uint32_t pix = heads[k].x;
+    b1::SplitPx &P = V.sp_px[pix];
+    if (last_round || !(P.o < P.len && P.s > 0 && P.s < spp)) continue;
+    const uint32_t r = spp - P.s, w = P.w, o = P.o;
+    const double mu = (double)o / (double)P.s;
+    const uint32_t run = (uint32_t)fmin((double)(P.len - o), ceil((double)r * mu * margin) + w);
+    int K = (int)fmin((double)kmax, ceil((double)r * P.cps / cstar));
+    K = (int)fmin((double)K, floor((double)run / (4.0 * w)));
+    if (K < 2) continue;  // a head chain through the rest
+    const uint32_t L = (run + K - 1) / K;
+    const uint32_t need = (uint32_t)(K - 1) * w;
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(n_items, need);
+    at = __shfl(at, 0);
+    const bool ok = at + need <= cap;
+    for (uint32_t q = lane; q < need; q += 64) {
+      if (at + q >= cap) break;
+      const uint32_t seg = 1u + q / w, t = q % w;
+      const uint32_t B = o + seg * L, E = seg + 1 == (uint32_t)K ? o + run : o + (seg + 1) * L;
+      items[at + q] = ok ? make_uint4(pix | b1::kSpecBit, B + t, E, 1u) : make_uint4(pix | b1::kSpecBit, 1u, 0u, 1u);
+    }
+    if (ok && lane == 0) {
+      P.stop_at = o + L;
+      P.len_run = o + run;
+    }
+  }
+}
+
+// Split render, after a round: follow each listed pixel's true chain through the sample records,
+// adding the colours in sample order (the reference's sum, src/raytracing.c:124).  A pixel whose
+// chain reaches spp samples is written; one that reaches an offset without a record (never
+// evaluated) is listed for the next round as a head chain from there.
+__global__ void split_walk_kernel(b1::Book1View V, uint8_t *__restrict__ out, const uint4 *in, const uint32_t *n_in,
+                                  uint4 *next, uint32_t *n_next, int last_round) {
+  const uint32_t n = *n_in;
+  const uint32_t spp = (uint32_t)V.S.cam.spp;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const uint32_t pix = in[k].x & ~b1::kSpecBit;
+    b1::SplitPx &P = V.sp_px[pix];
+    uint32_t s = P.s, o = P.o;
+    if (s >= spp) continue;  // written by its head chain
+    const uint32_t base = P.base, len = P.len;
+    f3 acc = mk(P.acc[0], P.acc[1], P.acc[2]);
+    while (s < spp && o < len && V.sp_claim[base + o] != 0u) {
+      const float4 r = V.sp_rec[base + o];
+      acc = add(acc, mk(r.x, r.y, r.z));
+      o += __float_as_uint(r.w);
+      s++;
+    }
+    if (s == spp) {
+      b1::write_pixel(out + (size_t)pix * 3, acc, (int)spp);
+      P.s = spp;
+    } else {
+      P.acc[0] = acc.x, P.acc[1] = acc.y, P.acc[2] = acc.z;
+      P.o = o, P.s = s;
+      P.stop_at = last_round ? b1::kNoCoalesce : b1::kNoStop;  // a head chain that stops at a claimed offset
+      next[atomicAdd(n_next, 1u)] = make_uint4(pix, 0u, 0u, 0u);
+    }
+  }
 }
 
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
@@ -350,6 +442,25 @@ struct rt_device_scene {
   size_t g_lds_bytes = 0;
   hipStream_t wave_stream = nullptr;  // the whole-wave kernel's stream (forked from / joined to the caller's)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // split render (rt_book1.h: SplitPx), RT_SPLIT: 0 off (default), 1 every LPT launch, 2 launches with fewer
+  // pixels than lanes
+  int split_mode = 0;
+  float split_beta = 0.7f;    // a chain's target cost, as a fraction of the frame's throughput time
+  float split_margin = 1.1f;  // first-round chains cover this times the pre-pass estimate of the stream length
+  float split_alloc = 2.0f;   // records per pixel: this times the estimate (a re-split continues into them)
+  float split_fixc = 0.25f;   // a re-split's chain target, as a fraction of the first round's
+  float split_wfact = 2.0f;   // window: this times the pre-pass draws per sample
+  int split_kmax = 64, split_rounds = 3;
+  uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
+  void *sp_arena = nullptr;
+  size_t sp_bytes = 0;
+  std::vector<uint32_t> h_cost, h_draws;
+  std::vector<b1::SplitPx> h_px;
+  std::vector<uint4> h_items, h_walk;
+  std::vector<uint32_t> h_pre;
+  uint32_t h_cnt[256];  // device counters: [0] chains, [1] split pixels, [2 + r] / [128 + r] round r's
+  int split_rounds_used = 0;
+  int sp_grid = 0;  // resident workgroups of rt_book1_split_kernel
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -763,17 +874,18 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const int spill_lanes = d->b1_grid * b1::kBlock;
   const size_t spill_bytes = (size_t)(kMaxDepth / 4) * spill_lanes * sizeof(uint64_t);  // Record chunks
 
-  size_t off[15], total = 0;
+  size_t off[16], total = 0;
   const size_t cost_bytes = d->book1_stats ? (size_t)s->camera.width * s->camera.height * 2 * sizeof(uint32_t) : 0;
-  const size_t sizes[15] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
+  const size_t sizes[16] = {nodes.size() * sizeof(float4), sph.size() * sizeof(float4), mats.size() * sizeof(b1::FastMat),
                            roots.size() * sizeof(uint16_t), 256, spill_bytes, cost_bytes,  // [4]: counter + stats
                            nodes7.size() * sizeof(float4), roots7.size() * sizeof(uint16_t),
                            items9.size() * sizeof(float4),
                            (size_t)s->camera.width * s->camera.height * sizeof(uint32_t),   // [10] LPT cost
                            (size_t)s->camera.width * s->camera.height * sizeof(int32_t),    // [11] LPT order
                            kLptHistBytes,                                                    // [12] LPT buckets
-                           wide.size() * sizeof(uint4), anc.size() * sizeof(uint16_t)};      // [13] [14] group
-  for (int k = 0; k < 15; k++) {
+                           wide.size() * sizeof(uint4), anc.size() * sizeof(uint16_t),      // [13] [14] group
+                           (size_t)s->camera.width * s->camera.height * sizeof(uint32_t)};  // [15] pre-pass draws
+  for (int k = 0; k < 16; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -839,6 +951,37 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
   d->lpt_cost = (uint32_t *)(b + off[10]);
   d->lpt_order = (int32_t *)(b + off[11]);
   d->lpt_hist = (uint32_t *)(b + off[12]);
+  d->draw_out = (uint32_t *)(b + off[15]);
+  {
+    int per = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)rt_book1_split_kernel<true>, b1::kBlock,
+                                                        d->b1_lds_bytes));
+    d->sp_grid = prop.multiProcessorCount * (per < 1 ? 1 : per);
+    if (d->sp_grid > d->b1_grid) d->sp_grid = d->b1_grid;  // the record spill area has b1_grid columns
+  }
+  V.draw_out = d->draw_out;
+  V.sp_px = nullptr;
+  V.sp_claim = nullptr;
+  V.sp_rec = nullptr;
+  V.sp_items = nullptr;
+  V.sp_n_items = nullptr;
+  {
+    const char *e = getenv("RT_SPLIT");
+    d->split_mode = (e && *e) ? atoi(e) : 0;  // opt-in: measured no faster than the group kernel
+    if (d->book1_ver != 9 || !d->book1_lds || d->book1_stats) d->split_mode = 0;
+    if ((e = getenv("RT_SPLIT_BETA")) && *e) d->split_beta = (float)atof(e);
+    if ((e = getenv("RT_SPLIT_MARGIN")) && *e) d->split_margin = (float)atof(e);
+    if ((e = getenv("RT_SPLIT_ALLOC")) && *e) d->split_alloc = (float)atof(e);
+    if ((e = getenv("RT_SPLIT_FIXC")) && *e) d->split_fixc = (float)atof(e);
+    if ((e = getenv("RT_SPLIT_W")) && *e) d->split_wfact = (float)atof(e);
+    if ((e = getenv("RT_SPLIT_KMAX")) && *e) d->split_kmax = atoi(e);
+    if ((e = getenv("RT_SPLIT_ROUNDS")) && *e) d->split_rounds = atoi(e);
+    if (d->split_kmax < 1) d->split_kmax = 1;
+    if (d->split_rounds < 1) d->split_rounds = 1;
+    if (d->split_rounds > 16) d->split_rounds = 16;
+    if (d->split_margin < 0.5f) d->split_margin = 0.5f;
+    if (d->split_alloc < d->split_margin) d->split_alloc = d->split_margin;
+  }
   d->lpt = env_flag("RT_LPT", true) && (d->book1_ver == 9 || d->book1_ver == 5) && d->book1_occ == 0;
   {
     const char *el = getenv("RT_LPT_SPP");
@@ -1008,6 +1151,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->b1_arena) (void)hipFree(d->b1_arena);
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->px_time) (void)hipFree(d->px_time);
+  if (d->sp_arena) (void)hipFree(d->sp_arena);
   if (d->wave_stream) (void)hipStreamDestroy(d->wave_stream);
   if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
   if (d->ev_join) (void)hipEventDestroy(d->ev_join);
@@ -1067,6 +1211,210 @@ static int launch_book1(rt_device_scene *d, const b1::Book1View &V, uint8_t *d_o
   return 0;
 }
 
+// Split render of one launch (rt_book1.h: SplitPx).  A pre-pass at lpt_spp measures each pixel's
+// traversal steps and pcg32 draws; the host cuts every pixel whose chain would outlast the frame's
+// throughput time into segments (and orders all chains longest first); then one round of chains,
+// the walk, and split_rounds fix-up rounds, all queued on the stream.  Returns 1 (nothing launched
+// after the pre-pass) when the plan does not fit its limits; the caller renders unsplit.
+static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
+  {
+    b1::Book1View P = V;
+    P.S.cam.spp = d->lpt_spp;
+    P.cost_out = d->lpt_cost;
+    P.draw_out = d->draw_out;
+    if (launch_book1(d, P, d_out, st, true) != 0) return -1;
+  }
+  const size_t n = (size_t)npix;
+  d->h_cost.resize(n);
+  d->h_draws.resize(n);
+  HIP_OK(hipMemcpyAsync(d->h_cost.data(), d->lpt_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(d->h_draws.data(), d->draw_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const double ratio = (double)V.S.cam.spp / (double)d->lpt_spp;
+  double sum = 0.0;
+  for (size_t p = 0; p < n; p++) sum += (double)d->h_cost[p];
+  // a chain's target cost (pre-pass steps): its latency at kLaneLat per step against the lanes'
+  // throughput time for the whole launch at kLaneThr per step
+  const double lanes = (double)d->sp_grid * b1::kBlock;
+  const double cstar = fmax(1.0, d->split_beta * sum * kLaneThr / (lanes * kLaneLat));
+  std::vector<b1::SplitPx> &px = d->h_px;
+  px.resize(n);
+  std::vector<uint16_t> kseg(n);
+  uint32_t hist[256] = {0};
+  uint64_t n_items = 0, rec_total = 0;
+  d->h_walk.clear();
+  for (size_t p = 0; p < n; p++) {
+    const double c = (double)d->h_cost[p];
+    int K = (int)fmin((double)d->split_kmax, ceil(c / cstar));
+    b1::SplitPx &P = px[p];
+    P.acc[0] = P.acc[1] = P.acc[2] = 0.0f;
+    P.o = P.s = 0u;
+    P.stop_at = b1::kNoCoalesce;
+    P.base = P.len = P.len_run = 0u;
+    const double mu = fmax(1.0, (double)d->h_draws[p] / d->lpt_spp);  // draws per sample
+    const uint32_t w = (uint32_t)fmin(512.0, fmax(8.0, ceil(d->split_wfact * mu)));
+    P.w = w;
+    P.cps = (float)(c / V.S.cam.spp);  // pre-pass steps per frame sample
+    P.rec_lo = 0xffffffffu;
+    const double est = (double)d->h_draws[p] * ratio;
+    const double len = ceil(est * d->split_margin) + w;
+    if (K > 1) K = (int)fmin((double)K, floor(len / (4.0 * w)));  // segments of at least 4 windows
+    if (K < 2) K = 1;
+    kseg[p] = (uint16_t)K;
+    if (K > 1) {
+      const uint32_t L = (uint32_t)ceil(len / K);
+      P.len_run = (uint32_t)len;
+      P.len = (uint32_t)fmax(len, ceil(est * d->split_alloc) + 2.0 * w);
+      P.stop_at = L;
+      P.rec_lo = L;
+      P.base = (uint32_t)(rec_total - L);  // records of offsets [L, len) only (u32 wrap-around)
+      rec_total += P.len - L;
+      d->h_walk.push_back(make_uint4((uint32_t)p, 0u, 0u, 0u));
+    }
+    const uint32_t b = host_lpt_bucket((uint32_t)fmin(4294967295.0, c / K));
+    hist[b] += (uint32_t)K;
+    n_items += (uint64_t)K;
+  }
+  if (rec_total >= ((uint64_t)15 << 28) || n_items >= ((uint64_t)1 << 31)) {  // u32 record indices
+    if (env_flag("RT_DEBUG", false)) fprintf(stderr, "[rtc] split: plan too large (%llu records), unsplit\n", (unsigned long long)rec_total);
+    return 1;
+  }
+  const uint64_t n_ent = n_items;
+  // longest chains first: bucket offsets from the top bucket down
+  uint32_t start[256];
+  for (int k = 255, run = 0; k >= 0; k--) start[k] = (uint32_t)run, run += (int)hist[k];
+  d->h_items.resize((size_t)n_items);  // entries: heads, and one per segment window
+  for (size_t p = 0; p < n; p++) {
+    const int K = kseg[p];
+    const uint32_t b = host_lpt_bucket((uint32_t)fmin(4294967295.0, (double)d->h_cost[p] / K));
+    d->h_items[start[b]++] = make_uint4((uint32_t)p, 0u, 0u, 0u);
+    if (K > 1) {
+      const b1::SplitPx &P = px[p];
+      const uint32_t L = P.stop_at;
+      const uint32_t w = (uint32_t)fmin(512.0, fmax(8.0, ceil(d->split_wfact * fmax(1.0, (double)d->h_draws[p] / d->lpt_spp))));
+      for (int k = 1; k < K; k++) {
+        const uint32_t B = (uint32_t)k * L, E = k + 1 == K ? P.len_run : (uint32_t)(k + 1) * L;
+        d->h_items[start[b]++] = make_uint4((uint32_t)p | b1::kSpecBit, B, E, w);
+      }
+    }
+  }
+  const size_t n_split = d->h_walk.size();
+  d->h_pre.resize((size_t)n_ent);
+  uint64_t n_chains = 0;
+  for (size_t e = 0; e < (size_t)n_ent; e++) d->h_pre[e] = (uint32_t)n_chains, n_chains += d->h_items[e].w ? d->h_items[e].w : 1u;
+  if (n_chains >= ((uint64_t)1 << 31)) return 1;
+  // device buffers: px, items, walk list, two fix-up lists, counters, claims, records
+  size_t off[10], total = 0;
+  const size_t sizes[10] = {n * sizeof(b1::SplitPx), (size_t)n_chains * sizeof(uint4), (n_split + 1) * sizeof(uint4),
+                           2 * (n_split + 1) * sizeof(uint4), 256 * sizeof(uint32_t),
+                           (size_t)rec_total * sizeof(uint32_t), (size_t)rec_total * sizeof(float4),
+                           (size_t)n_ent * sizeof(uint4), (size_t)n_ent * sizeof(uint32_t),
+                           (size_t)n_chains * sizeof(uint4)};  // [9] re-split chains of a fix-up round
+  for (int k = 0; k < 10; k++) off[k] = total, total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
+  if (total > d->sp_bytes) {
+    if (d->sp_arena) HIP_OK(hipFree(d->sp_arena));
+    d->sp_arena = nullptr;
+    d->sp_bytes = 0;
+    HIP_OK(hipMalloc(&d->sp_arena, total));
+    d->sp_bytes = total;
+  }
+  char *b = (char *)d->sp_arena;
+  uint32_t *cnt = (uint32_t *)(b + off[4]);
+  d->h_cnt[0] = (uint32_t)n_chains;
+  d->h_cnt[1] = (uint32_t)n_split;
+  for (int k = 2; k < 256; k++) d->h_cnt[k] = 0u;
+  HIP_OK(hipMemcpyAsync(b + off[0], px.data(), sizes[0], hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(b + off[7], d->h_items.data(), sizes[7], hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(b + off[8], d->h_pre.data(), sizes[8], hipMemcpyHostToDevice, st));
+  {
+    const unsigned eb = (unsigned)(n_ent / 256 + 1 < 4096 ? n_ent / 256 + 1 : 4096);
+    hipLaunchKernelGGL(split_expand_kernel, dim3(eb), dim3(256), 0, st, (const uint4 *)(b + off[7]),
+                       (const uint32_t *)(b + off[8]), (uint32_t)n_ent, (uint4 *)(b + off[1]));
+    HIP_OK(hipGetLastError());
+  }
+  if (n_split) HIP_OK(hipMemcpyAsync(b + off[2], d->h_walk.data(), n_split * sizeof(uint4), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(cnt, d->h_cnt, 256 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (env_flag("RT_DEBUG", false))
+    fprintf(stderr, "[rtc] split: %zu px, %zu split, %llu entries, %llu chains, %llu records (%.1f MB), chain target %.0f steps\n", n,
+            n_split, (unsigned long long)n_ent, (unsigned long long)n_chains, (unsigned long long)rec_total, total / 1e6, cstar * ratio);
+  if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+  if (rec_total) HIP_OK(hipMemsetAsync(b + off[5], 0, sizes[5], st));
+  V.sp_px = (b1::SplitPx *)(b + off[0]);
+  V.sp_claim = (uint32_t *)(b + off[5]);
+  V.sp_rec = (float4 *)(b + off[6]);
+  V.order = nullptr;
+  V.n_coop = nullptr;
+  V.n_heavy = nullptr;
+  V.cost_out = nullptr;
+  V.sp_items2 = nullptr;
+  V.sp_n_items2 = nullptr;
+  V.sp_cap2 = 0u;
+  uint4 *items2 = (uint4 *)(b + off[9]);
+  uint4 *walk0 = (uint4 *)(b + off[2]);
+  uint4 *fix[2] = {(uint4 *)(b + off[3]), (uint4 *)(b + off[3]) + (n_split + 1)};
+  const dim3 gs((unsigned)d->sp_grid), blk(b1::kBlock);
+  const unsigned wb = (unsigned)(n_split / 256 + 1 < 2048 ? n_split / 256 + 1 : 2048);
+  const int rounds = d->split_rounds;
+  const bool dbg = env_flag("RT_DEBUG", false);
+  auto dbg_mark = [&](const char *what, int r) {  // diagnostic: synchronous timing of each step
+    static double t_last = 0.0;
+    (void)hipStreamSynchronize(st);
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double t = ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+    uint32_t c[136];
+    (void)hipMemcpy(c, cnt, sizeof c, hipMemcpyDeviceToHost);
+    if (what) fprintf(stderr, "[rtc] split %s %d: %.2f ms (counts %u %u | fix %u %u %u %u | resplit %u %u %u)\n", what, r,
+                      t - t_last, c[0], c[1], c[2], c[3], c[4], c[5], c[129], c[130], c[131]);
+    t_last = t;
+  };
+  if (dbg) dbg_mark(nullptr, 0);
+  // round r: (r > 0: re-split the unfinished pixels) chains, then the walk; its unfinished pixels are
+  // round r+1's heads.  The first `rounds` rounds are queued without a host sync; then the host
+  // checks the count and queues more while pixels remain; round kMaxRounds-1 walks with
+  // last_round set, so round kMaxRounds's heads run to the end without stopping.
+  constexpr int kMaxRounds = 100;
+  auto queue_round = [&](int r) -> int {
+    V.sp_items = r == 0 ? (const uint4 *)(b + off[1]) : fix[(r - 1) % 2];
+    V.sp_n_items = r == 0 ? cnt : cnt + 1 + r;
+    if (r > 0) {  // re-split pixels' segment chains (split_replan_kernel, counter cnt[128 + r])
+      hipLaunchKernelGGL(split_replan_kernel, dim3(wb), dim3(256), 0, st, V, fix[(r - 1) % 2], cnt + 1 + r, items2,
+                         cnt + 128 + r, (uint32_t)n_chains, (float)(cstar * d->split_fixc), d->split_margin,
+                         d->split_kmax, (int)(r == kMaxRounds));
+      HIP_OK(hipGetLastError());
+      V.sp_items2 = items2;
+      V.sp_n_items2 = cnt + 128 + r;
+      V.sp_cap2 = (uint32_t)n_chains;
+      if (dbg) dbg_mark("replan", r);
+    }
+    HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(rt_book1_split_kernel<true>, gs, blk, d->b1_lds_bytes, st, V, d_out);
+    HIP_OK(hipGetLastError());
+    if (dbg) dbg_mark("chains", r);
+    if (r < kMaxRounds) {  // the walk over this round's split pixels; misses become next round's heads
+      hipLaunchKernelGGL(split_walk_kernel, dim3(wb), dim3(256), 0, st, V, d_out, r == 0 ? walk0 : fix[(r - 1) % 2],
+                         r == 0 ? cnt + 1 : cnt + 1 + r, fix[r % 2], cnt + 2 + r, (int)(r + 1 == kMaxRounds));
+      HIP_OK(hipGetLastError());
+      if (dbg) dbg_mark("walk", r);
+    }
+    return 0;
+  };
+  int r = 0;
+  for (; r <= rounds && r <= kMaxRounds; r++)
+    if (queue_round(r) != 0) return -1;
+  while (n_split && r <= kMaxRounds) {  // more rounds while the last walk left pixels unfinished
+    uint32_t left = 0;
+    HIP_OK(hipMemcpyAsync(&left, cnt + 1 + r, sizeof left, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (left == 0) break;
+    if (queue_round(r) != 0) return -1;
+    r++;
+  }
+  d->split_rounds_used = r;
+  if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+  return 0;
+}
+
 extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out,
                                     void *stream) {
   if (!d || !d_out) return rt_set_error("rt_render_rows_async: NULL argument"), -1;
@@ -1087,6 +1435,12 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     // over several GPUs): there the sequential per-pixel chains, not the lanes' throughput, set the time
     const bool use_group =
         d->group_mode == 1 || (d->group_mode == 2 && npix < (int64_t)d->b1_grid * b1::kBlock);
+    // the split render where the chains, not the lanes, bound the launch (RT_SPLIT)
+    if (d->split_mode != 0 && d->lpt && V.S.cam.spp >= 4 * d->lpt_spp && npix >= 4096 && V.S.cam.max_depth >= 1 &&
+        (d->split_mode == 1 || npix < (int64_t)d->b1_grid * b1::kBlock)) {
+      const int rc = launch_split(d, V, d_out, st, npix);
+      if (rc <= 0) return rc;
+    }
     // longest-first order: a low-spp pass measures each work item's traversal steps
     if (d->lpt && V.S.cam.spp >= 4 * d->lpt_spp && npix >= 4096) {
       b1::Book1View P = V;

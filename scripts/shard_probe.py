@@ -19,6 +19,7 @@ st = torch.cuda.current_stream()
 
 
 def time_rows(row0, stride, n, reps=2):
+    global last
     buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda")
     ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)  # warm-up
     torch.cuda.synchronize()
@@ -29,10 +30,12 @@ def time_rows(row0, stride, n, reps=2):
         torch.cuda.synchronize()
         best = min(best, time.perf_counter() - t0)
         kbest = min(kbest, ds.last_launch_ms())
+    last = buf.cpu().numpy()
     return best, kbest
 
 
 t1, k1 = time_rows(0, 1, sc.height)
+full = last
 print(f"world=1 ms={t1 * 1e3:.1f} kernel_ms={k1:.1f} Msamples/s={sc.width * sc.height * spp / t1 / 1e6:.0f}", flush=True)
 for world in worlds:
     ranks = range(world) if ranks_arg == "all" else [int(r) for r in ranks_arg.split(",")]
@@ -41,7 +44,8 @@ for world in worlds:
         row0, stride, n = rtc.rows_of(sc.height, rank, world)
         t, k = time_rows(row0, stride, n)
         worst = max(worst, t)
-        print(f"  world={world} rank={rank} rows={n} ms={t * 1e3:.1f} kernel_ms={k:.1f}", flush=True)
+        same = bool((last == full[row0::stride][:n]).all())  # rows identical to the 1-GPU frame
+        print(f"  world={world} rank={rank} rows={n} ms={t * 1e3:.1f} kernel_ms={k:.1f} identical={same}", flush=True)
     print(f"world={world} max_ms={worst * 1e3:.1f} frame_Msamples/s={sc.width * sc.height * spp / worst / 1e6:.0f} "
           f"scale={t1 / worst:.2f}x", flush=True)
 ds.close()

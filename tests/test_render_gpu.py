@@ -145,7 +145,13 @@ def test_cli_rt_main_matches_golden(manifest, tmp_path):
                                  {"RT_MODE": "group", "RT_LPT": "0"}, {"RT_MODE": "lane", "RT_LPT_SPP": "1"},
                                  {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024"},
                                  {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024", "RT_BF": "0"}, {"RT_COOP_LANES": "64"}, {"RT_COOP_LANES": "0"}, {"RT_SHADE_BATCH": "1"},
-                                 {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"}])
+                                 {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"},
+                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1"},
+                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001"},
+                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001", "RT_SPLIT_W": "0.2"},
+                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001", "RT_SPLIT_W": "0.2",
+                                  "RT_SPLIT_MARGIN": "1.0", "RT_SPLIT_ROUNDS": "1"},
+                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "2", "RT_SPLIT_BETA": "0.01", "RT_SPLIT_KMAX": "3"}])
 @pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
 def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
     """Book-1 scenes run on the persistent fast kernel (LDS or global geometry) unless RT_BOOK1=0
@@ -161,3 +167,17 @@ def test_book1_deep_paths_spill(monkeypatch):
     """max_depth 64 with a glass-heavy view: paths longer than the register record spill to HBM."""
     sc = rtc.Scene.preset(1, 160, 24, 64)
     _check(rtc.render(sc), pyoracle.render(sc), "scene 1 depth 64")
+
+
+@pytest.mark.parametrize("env", [{}, {"RT_SPLIT_BETA": "0.002"}, {"RT_SPLIT_BETA": "0.002", "RT_SPLIT_W": "0.2", "RT_SPLIT_MARGIN": "1.0"}])
+def test_split_render_north_star_scene(manifest, env, monkeypatch):
+    """Stream-split render (rt_book1.h: SplitPx) forced on the Book-1 final scene at full size: pixels
+    cut into segments of their pcg32 stream, windows of speculative chains, the walk and the fix-up
+    rounds must reproduce the reference frame bit for bit."""
+    monkeypatch.setenv("RT_SPLIT", "1")
+    monkeypatch.setenv("RT_LPT_SPP", "2")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = manifest["renders"]["s1_1200x675_10spp_d50"]
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"], env
