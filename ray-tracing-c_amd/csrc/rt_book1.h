@@ -62,6 +62,8 @@ struct SplitPx {            // 48 B per work item of a split launch
 constexpr uint32_t kNoStop = 0xffffffffu;      // stop at a claimed offset only (fix-up rounds)
 constexpr uint32_t kNoCoalesce = 0xfffffffeu;  // never stop before spp samples (unsplit pixels, last round)
 constexpr uint32_t kSpecBit = 0x80000000u;     // sp_items[].x: segment item (else head item)
+constexpr uint32_t kRecFill = 0xffffffffu;     // sp_rec words before their record is written (a NaN no
+                                               // arithmetic produces; the draw count is never this)
 
 struct Book1View {
   DScene S;                  // full scene (global memory): sphere aux data, camera
@@ -1353,7 +1355,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       t_iter = now;
     }
     if ((trav | wait) == 0) break;
-    if (n_heavy > 0) {  // the longest pixels' waves issue first: their chains set the frame time
+    if (n_heavy > 0 || (kMode == 2 && V.experiment == 1)) {  // the longest pixels' waves issue first: their chains set the frame time
       const bool want_prio = __ballot(heavy && mode != kExit) != 0;
       if (want_prio != prio) {
         prio = want_prio;
@@ -1459,8 +1461,15 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       }
       if (kMode == 2 && path_done) {  // split render: the chain check below decides what follows
         const f3 col = rec_fold(V, R, tail, glane);
-        if (spec) {
-          V.sp_rec[V.sp_px[pix].base + so] = make_float4(col.x, col.y, col.z, __uint_as_float(g.n - so));
+        if (spec) {  // the record, then claim 2 (relaxed device-coherent stores: no cache maintenance;
+                     // a reader that sees claim 2 before all four words checks them for the fill value)
+          const uint32_t at = V.sp_px[pix].base + so;
+          uint32_t *rw = (uint32_t *)(V.sp_rec + at);
+          __hip_atomic_store(rw + 0, __float_as_uint(col.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rw + 1, __float_as_uint(col.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rw + 2, __float_as_uint(col.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rw + 3, g.n - so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&V.sp_claim[at], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
           acc = add(acc, col);
           s++;
@@ -1503,6 +1512,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           it = pix < n_items1 ? V.sp_items[pix] : V.sp_items2[pix - n_items1];
           spec = (it.x & kSpecBit) != 0u;
           pix = (int64_t)(it.x & ~kSpecBit);
+          heavy = !spec && V.sp_px[pix].len != 0u;  // a split pixel's head: the critical chain
         } else {
           heavy = pix + work_offset < n_heavy;
           if (V.order) pix = V.order[pix + work_offset];  // longest work items first
@@ -1532,20 +1542,39 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       if (kMode == 2) {  // the chain check at a sample boundary
         const uint32_t sbase = V.sp_px[pix].base, slen = V.sp_px[pix].len, srec_lo = V.sp_px[pix].rec_lo;
         if (!spec) {
+          // the head is the pixel's true chain: it takes the samples segment chains have finished
+          // (claim 2: record written) in order, and computes any other itself -- claiming a free
+          // offset first, so segment chains that reach it stop there.  (Records exist only past
+          // segment 0: sbase + o is a valid index for o >= rec_lo.)
+          if (send != kNoCoalesce) {
+            for (;;) {
+              if (s == spp || !(so >= srec_lo && so < slen)) break;
+              uint32_t *cl = &V.sp_claim[sbase + so];
+              const uint32_t c = __hip_atomic_load(cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              uint32_t rx = kRecFill, ry = kRecFill, rz = kRecFill, rd = kRecFill;
+              if (c == 2u) {
+                const uint32_t *rw = (const uint32_t *)(V.sp_rec + (uint32_t)(sbase + so));  // u32 index (wraps)
+                rx = __hip_atomic_load(rw + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ry = __hip_atomic_load(rw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rz = __hip_atomic_load(rw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rd = __hip_atomic_load(rw + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              if (rx == kRecFill || ry == kRecFill || rz == kRecFill || rd == kRecFill) {
+                if (c == 0u) (void)atomicCAS(cl, 0u, 1u);  // free: this chain computes it (others stop here)
+                break;
+              }
+              acc = add(acc, mk(__uint_as_float(rx), __uint_as_float(ry), __uint_as_float(rz)));
+              so += rd;
+              s++;
+            }
+          }
           if (s == spp) {  // the pixel's last sample: quantize (src/raytracing.c:127-131)
             write_pixel(out + pix * 3, acc, spp);
             V.sp_px[pix].s = (uint32_t)spp;
             need_pixel = true;
             continue;
           }
-          // (records exist only past segment 0: sbase + o is a valid index for o >= segment 0's end)
-          if (so >= send || (send != kNoCoalesce && so >= srec_lo && so < slen && V.sp_claim[sbase + so] != 0u)) {
-            SplitPx &P = V.sp_px[pix];  // segment 0 done, or joined evaluated records: the walk goes on
-            P.acc[0] = acc.x, P.acc[1] = acc.y, P.acc[2] = acc.z;
-            P.o = so, P.s = (uint32_t)s;
-            need_pixel = true;
-            continue;
-          }
+          g.skip(so - g.n);  // past the samples taken from records
         } else if (!(so < send && so < slen && atomicCAS(&V.sp_claim[sbase + so], 0u, 1u) == 0u)) {
           need_pixel = true;  // a chain ends at its segment's end or at an offset another chain owns
           continue;

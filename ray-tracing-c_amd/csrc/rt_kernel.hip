@@ -170,8 +170,8 @@ __global__ void split_walk_kernel(b1::Book1View V, uint8_t *__restrict__ out, co
     if (s >= spp) continue;  // written by its head chain
     const uint32_t base = P.base, len = P.len;
     f3 acc = mk(P.acc[0], P.acc[1], P.acc[2]);
-    while (s < spp && o < len && V.sp_claim[base + o] != 0u) {
-      const float4 r = V.sp_rec[base + o];
+    while (s < spp && o < len && V.sp_claim[base + o] == 2u) {
+      const float4 r = V.sp_rec[base + o];  // (after the round's kernel: every claimed record is complete)
       acc = add(acc, mk(r.x, r.y, r.z));
       o += __float_as_uint(r.w);
       s++;
@@ -447,10 +447,10 @@ struct rt_device_scene {
   int split_mode = 0;
   float split_beta = 0.7f;    // a chain's target cost, as a fraction of the frame's throughput time
   float split_margin = 1.1f;  // first-round chains cover this times the pre-pass estimate of the stream length
-  float split_alloc = 2.0f;   // records per pixel: this times the estimate (a re-split continues into them)
+  float split_alloc = 1.0f;   // records per pixel: this times the estimate (a re-split continues into them)
   float split_fixc = 0.25f;   // a re-split's chain target, as a fraction of the first round's
   float split_wfact = 2.0f;   // window: this times the pre-pass draws per sample
-  int split_kmax = 64, split_rounds = 3;
+  int split_kmax = 64, split_rounds = 0;  // rounds queued before the host checks (heads walk: usually none)
   uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
   void *sp_arena = nullptr;
   size_t sp_bytes = 0;
@@ -1287,8 +1287,7 @@ static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   for (size_t p = 0; p < n; p++) {
     const int K = kseg[p];
     const uint32_t b = host_lpt_bucket((uint32_t)fmin(4294967295.0, (double)d->h_cost[p] / K));
-    d->h_items[start[b]++] = make_uint4((uint32_t)p, 0u, 0u, 0u);
-    if (K > 1) {
+    if (K > 1) {  // the segment windows first, then the head: the head walks the segments' records
       const b1::SplitPx &P = px[p];
       const uint32_t L = P.stop_at;
       const uint32_t w = (uint32_t)fmin(512.0, fmax(8.0, ceil(d->split_wfact * fmax(1.0, (double)d->h_draws[p] / d->lpt_spp))));
@@ -1297,6 +1296,7 @@ static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
         d->h_items[start[b]++] = make_uint4((uint32_t)p | b1::kSpecBit, B, E, w);
       }
     }
+    d->h_items[start[b]++] = make_uint4((uint32_t)p, 0u, 0u, 0u);
   }
   const size_t n_split = d->h_walk.size();
   d->h_pre.resize((size_t)n_ent);
@@ -1338,7 +1338,10 @@ static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
     fprintf(stderr, "[rtc] split: %zu px, %zu split, %llu entries, %llu chains, %llu records (%.1f MB), chain target %.0f steps\n", n,
             n_split, (unsigned long long)n_ent, (unsigned long long)n_chains, (unsigned long long)rec_total, total / 1e6, cstar * ratio);
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
-  if (rec_total) HIP_OK(hipMemsetAsync(b + off[5], 0, sizes[5], st));
+  if (rec_total) {
+    HIP_OK(hipMemsetAsync(b + off[5], 0, sizes[5], st));
+    HIP_OK(hipMemsetAsync(b + off[6], 0xff, sizes[6], st));  // kRecFill
+  }
   V.sp_px = (b1::SplitPx *)(b + off[0]);
   V.sp_claim = (uint32_t *)(b + off[5]);
   V.sp_rec = (float4 *)(b + off[6]);
