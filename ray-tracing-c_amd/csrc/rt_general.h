@@ -108,7 +108,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
     } else {
       Hit h;
       rays++;
-      if (!trace<F>(S, o, d, 1e-3f, g, h)) {
+      if (!(S.pre ? trace_pre<F>(S, o, d, 1e-3f, g, h) : trace<F>(S, o, d, 1e-3f, g, h))) {
         tail = ld3(S.cam.background);
         path_done = true;
       } else {

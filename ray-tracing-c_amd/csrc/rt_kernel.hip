@@ -461,6 +461,7 @@ struct rt_device_scene {
   uint32_t h_cnt[256];  // device counters: [0] chains, [1] split pixels, [2 + r] / [128 + r] round r's
   int split_rounds_used = 0;
   int sp_grid = 0;  // resident workgroups of rt_book1_split_kernel
+  void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1131,6 +1132,20 @@ extern "C" rt_device_scene *rt_scene_upload(const rt_flat_scene *s, int device) 
   const void *dev_arrays[13];
   for (int k = 0; k < 13; k++) dev_arrays[k] = (char *)arena + parts[k].off;
   d->view = make_view(*s, dev_arrays);
+  if (!book1_eligible(s) && env_flag("RT_GEN_PRE", true)) {  // the general path's preorder (trace_pre)
+    std::vector<float4> pre;
+    build_preorder(*s, pre);
+    if (!pre.empty()) {
+      if (hipMalloc(&d->pre_arena, pre.size() * sizeof(float4)) != hipSuccess ||
+          hipMemcpy(d->pre_arena, pre.data(), pre.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess) {
+        rt_set_error("preorder upload failed on device %d", device);
+        rt_scene_release(d);
+        return NULL;
+      }
+      d->view.pre = (const float4 *)d->pre_arena;
+      d->view.n_pre = (int32_t)(pre.size() / 2);
+    }
+  }
   if (hipEventCreate(&d->ev_main[0]) != hipSuccess || hipEventCreate(&d->ev_main[1]) != hipSuccess)
     d->ev_main[0] = d->ev_main[1] = nullptr;
   if (book1_eligible(s) && book1_upload(d, s) != 0) {
@@ -1152,6 +1167,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->px_time) (void)hipFree(d->px_time);
   if (d->sp_arena) (void)hipFree(d->sp_arena);
+  if (d->pre_arena) (void)hipFree(d->pre_arena);
   if (d->wave_stream) (void)hipStreamDestroy(d->wave_stream);
   if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
   if (d->ev_join) (void)hipEventDestroy(d->ev_join);

@@ -23,7 +23,8 @@ int main(int argc, char **argv) {
     fprintf(stderr, "preset failed: %s\n", rt_last_error());
     return 1;
   }
-  const bool force_all = argc > 6 && !strcmp(argv[6], "all");
+  const bool use_pre = argc > 6 && !strcmp(argv[6], "pre");  // preorder trace (trace_pre)
+  const bool force_all = argc > 6 && (!strcmp(argv[6], "all") || use_pre);
   const bool book1 = !force_all && (s->features & ~rt::kFeatBook1) == 0;
   if (s->stack_needed > rt::kStackMax || s->camera.max_depth > rt::kMaxDepth) {
     fprintf(stderr, "scene exceeds kernel limits\n");
@@ -32,7 +33,13 @@ int main(int argc, char **argv) {
   const void *arrays[13] = {s->bvh,        s->spheres,  s->quads,     s->lists,  s->list_items,
                             s->translates, s->rotates,  s->media,     s->materials, s->textures,
                             s->images,     s->perlins,  s->image_bytes};
-  const rt::DScene view = rt::make_view(*s, arrays);
+  rt::DScene view = rt::make_view(*s, arrays);
+  std::vector<float4> pre;
+  if (use_pre) {
+    rt::build_preorder(*s, pre);
+    view.pre = pre.data();
+    view.n_pre = (int32_t)(pre.size() / 2);
+  }
   const int W = s->camera.width, H = s->camera.height;
   std::vector<uint8_t> img((size_t)W * H * 3);
 #pragma omp parallel for schedule(dynamic, 16)
@@ -45,7 +52,7 @@ int main(int argc, char **argv) {
   FILE *f = fopen(argv[5], "wb");
   fwrite(img.data(), 1, img.size(), f);
   fclose(f);
-  printf("%d %d %s\n", W, H, book1 ? "book1" : "all");
+  printf("%d %d %s\n", W, H, book1 ? "book1" : use_pre ? "pre" : "all");
   rt_flat_free(s);
   return 0;
 }

@@ -21,14 +21,17 @@ EXE = os.path.join(ROOT, "tests", "native", "bin", "kernel_host_check")
 @pytest.mark.parametrize("scene,width,spp,depth,variant", [
     (0, 96, 4, 50, "book1"), (1, 96, 4, 50, "book1"), (1, 64, 3, 50, "all"), (2, 96, 3, 50, "all"),
     (3, 80, 3, 50, "all"), (4, 96, 3, 50, "all"), (5, 96, 6, 50, "all"), (6, 64, 4, 50, "all"),
-    (7, 80, 3, 50, "all"), (1, 33, 2, 1, "book1"), (7, 40, 2, 2, "all")])
+    (7, 80, 3, 50, "all"), (1, 33, 2, 1, "book1"), (7, 40, 2, 2, "all"),
+    (1, 64, 3, 50, "pre"), (2, 96, 3, 50, "pre"), (3, 80, 3, 50, "pre"), (4, 96, 3, 50, "pre"),
+    (5, 96, 6, 50, "pre"), (6, 64, 4, 50, "pre"), (7, 80, 3, 50, "pre"), (7, 40, 2, 2, "pre")])
 def test_kernel_code_on_host_matches_oracle(tmp_path, scene, width, spp, depth, variant):
+    """variant: book1 / all (stack trace) / pre (preorder trace_pre)"""
     out = str(tmp_path / "k.rgb")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", OMP_NUM_THREADS="8")
     r = subprocess.run([EXE, str(scene), str(width), str(spp), str(depth), out, variant], capture_output=True,
                        text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    assert r.stdout.split()[2] == (variant if scene > 1 or variant == "all" else "book1")
+    assert r.stdout.split()[2] == (variant if scene > 1 or variant in ("all", "pre") else "book1")
     sc = rtc.Scene.preset(scene, width, spp, depth)
     ref = pyoracle.render(sc)
     got = np.fromfile(out, np.uint8).reshape(ref.shape)
