@@ -375,7 +375,7 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
 // 2 float4, so trace_pre is a scan with skips, without a stack:
 //   BVH node:   q0 = (lo.x, lo.y, lo.z, hi.x)  q1 = (hi.y, hi.z, skip, ref)  next = hit ? p+1 : skip
 //   transform:  q0 = (end, -, enclosing transform's position or ~0, -)  q1 = (-, -, end, ref)
-//   primitive:  q1.w = ref (sphere, quad, medium)                          next = p+1
+//   sphere:     q0 = (center, r^2); quad: q0 = (normal, D); medium: -; q1.w = ref     next = p+1
 // (skip / end = the position after the subtree; integers stored as float bits).  Lists need no
 // entry.  Visit order, frames, t_max and rng draws (media) are the stack machine's.
 template <int F>
@@ -410,9 +410,11 @@ RT_D bool trace_pre(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h)
       nd.lo[0] = q0.x, nd.lo[1] = q0.y, nd.lo[2] = q0.z;
       nd.hi[0] = q0.w, nd.hi[1] = q1.x, nd.hi[2] = q1.y;
       if (!aabb_hit(nd, o, inv, tmin, tmax)) next = __builtin_bit_cast(uint32_t, q1.z);
-    } else if (kind == RT_KIND_SPHERE) {
+    } else if (kind == RT_KIND_SPHERE) {  // center and r^2 inline: no dependent load
       float t;
-      if (sphere_t(S.spheres[idx], o, d, dd, tmin, tmax, t)) {
+      rt_sphere sp;
+      sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
+      if (sphere_t(sp, o, d, dd, tmin, tmax, t)) {
         tmax = t;
         h.t = t;
         h.prim = ref;
@@ -420,8 +422,21 @@ RT_D bool trace_pre(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h)
         found = true;
       }
     } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
-      float t;
-      if (quad_t(S.quads[idx], o, d, tmin, tmax, t)) {
+      // quad_t with the plane (normal, D) inline: the quad record is read only past the plane test
+      const f3 nq = mk(q0.x, q0.y, q0.z);
+      const float denom = dot(nq, d);
+      const float tt = (q0.w - dot(nq, o)) / denom;
+      bool hit = !(fabsf(denom) < 1e-8f) && !((tt < tmin) || (tt > tmax));
+      if (hit) {
+        const rt_quad &qd = S.quads[idx];
+        const f3 hp = sub(ray_at(o, d, tt), ld3(qd.Q));
+        const f3 w = ld3(qd.w);
+        const float alpha = dot(w, cross(hp, ld3(qd.v)));
+        const float beta = dot(w, cross(ld3(qd.u), hp));
+        hit = !((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1));
+      }
+      if (hit) {
+        const float t = tt;
         tmax = t;
         h.t = t;
         h.prim = ref;
@@ -484,7 +499,15 @@ struct PreorderBuilder {
       for (int k = 0; k < l.count; k++) emit(s.list_items[l.first + k], enclosing);
       return;
     }
-    out.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (kind == RT_KIND_SPHERE) {
+      const rt_sphere &sp = s.spheres[idx];
+      q0 = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius_sq);
+    } else if (kind == RT_KIND_QUAD) {
+      const rt_quad &qd = s.quads[idx];
+      q0 = make_float4(qd.normal[0], qd.normal[1], qd.normal[2], qd.D);
+    }
+    out.push_back(q0);
     out.push_back(make_float4(0.0f, 0.0f, 0.0f, b((uint32_t)ref)));
     if (kind == RT_KIND_BVH) {
       const rt_bvh_node &nd = s.bvh[idx];
