@@ -378,105 +378,118 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
 //   sphere:     q0 = (center, r^2); quad: q0 = (normal, D); medium: -; q1.w = ref     next = p+1
 // (skip / end = the position after the subtree; integers stored as float bits).  Lists need no
 // entry.  Visit order, frames, t_max and rng draws (media) are the stack machine's.
+// The scan's state, so that a caller can run it a few entries at a time (rt_general.h).
+struct PreTrace {
+  f3 o, d, inv;            // the ray in the current frame
+  float dd, tmax;
+  int32_t frame;
+  uint32_t p, fend, fpos;  // next entry; the current frame's subtree end and entry position
+  bool found;
+  Hit h;
+};
+RT_D void pre_begin(PreTrace &T, f3 wo, f3 wd) {
+  T.o = wo, T.d = wd;
+  T.inv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
+  T.dd = dot(wd, wd);
+  T.tmax = __builtin_inff();
+  T.frame = RT_REF_NONE;
+  T.p = 0u, T.fend = 0xffffffffu, T.fpos = 0u;
+  T.found = false;
+}
+// One entry of the scan; returns true once the scan is past the last entry.
 template <int F>
-RT_D bool trace_pre(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
-  float tmax = __builtin_inff();
-  bool found = false;
-  int32_t frame = RT_REF_NONE;
-  uint32_t fend = 0xffffffffu, fpos = 0u;  // the current frame's subtree end and entry position
-  f3 o = wo, d = wd;
-  f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  float dd = dot(d, d);
+RT_D bool pre_step(const DScene &S, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g) {
   const uint32_t n = (uint32_t)S.n_pre;
-  for (uint32_t p = 0; p < n;) {
-    if (F & RT_FEAT_XFORM) {
-      while (p >= fend) {  // leaving a transform's subtree: the enclosing frame again
-        const uint32_t pp = __builtin_bit_cast(uint32_t, S.pre[2 * fpos].z);
-        frame = parent_of(S, frame);
-        fend = pp == 0xffffffffu ? 0xffffffffu : __builtin_bit_cast(uint32_t, S.pre[2 * pp].x);
-        fpos = pp == 0xffffffffu ? 0u : pp;
-        local_ray(S, frame, wo, wd, o, d);
-        inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        dd = dot(d, d);
-      }
+  if (T.p >= n) return true;
+  if (F & RT_FEAT_XFORM) {
+    while (T.p >= T.fend) {  // leaving a transform's subtree: the enclosing frame again
+      const uint32_t pp = __builtin_bit_cast(uint32_t, S.pre[2 * T.fpos].z);
+      T.frame = parent_of(S, T.frame);
+      T.fend = pp == 0xffffffffu ? 0xffffffffu : __builtin_bit_cast(uint32_t, S.pre[2 * pp].x);
+      T.fpos = pp == 0xffffffffu ? 0u : pp;
+      local_ray(S, T.frame, wo, wd, T.o, T.d);
+      T.inv = mk(1.0f / T.d.x, 1.0f / T.d.y, 1.0f / T.d.z);
+      T.dd = dot(T.d, T.d);
     }
-    const float4 q0 = S.pre[2 * p], q1 = S.pre[2 * p + 1];
-    const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
-    const int kind = rt_ref_kind(ref);
-    const int32_t idx = rt_ref_index(ref);
-    uint32_t next = p + 1;
-    if ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) {
-      rt_bvh_node nd;
-      nd.lo[0] = q0.x, nd.lo[1] = q0.y, nd.lo[2] = q0.z;
-      nd.hi[0] = q0.w, nd.hi[1] = q1.x, nd.hi[2] = q1.y;
-      if (!aabb_hit(nd, o, inv, tmin, tmax)) next = __builtin_bit_cast(uint32_t, q1.z);
-    } else if (kind == RT_KIND_SPHERE) {  // center and r^2 inline: no dependent load
-      float t;
-      rt_sphere sp;
-      sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
-      if (sphere_t(sp, o, d, dd, tmin, tmax, t)) {
-        tmax = t;
-        h.t = t;
-        h.prim = ref;
-        h.xform = frame;
-        found = true;
-      }
-    } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
-      // quad_t with the plane (normal, D) inline: the quad record is read only past the plane test
-      const f3 nq = mk(q0.x, q0.y, q0.z);
-      const float denom = dot(nq, d);
-      const float tt = (q0.w - dot(nq, o)) / denom;
-      bool hit = !(fabsf(denom) < 1e-8f) && !((tt < tmin) || (tt > tmax));
-      if (hit) {
-        const rt_quad &qd = S.quads[idx];
-        const f3 hp = sub(ray_at(o, d, tt), ld3(qd.Q));
-        const f3 w = ld3(qd.w);
-        const float alpha = dot(w, cross(hp, ld3(qd.v)));
-        const float beta = dot(w, cross(ld3(qd.u), hp));
-        hit = !((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1));
-      }
-      if (hit) {
-        const float t = tt;
-        tmax = t;
-        h.t = t;
-        h.prim = ref;
-        h.xform = frame;
-        found = true;
-      }
-    } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
-      frame = ref;
-      fend = __builtin_bit_cast(uint32_t, q0.x);
-      fpos = p;
-      local_ray(S, frame, wo, wd, o, d);
-      inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-      dd = dot(d, d);
-    } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
-      // ConstantMedium_hit (src/hittable.c:392-423): two boundary hits, clamp, one rng draw
-      const rt_medium m = S.media[idx];
-      float t1, t2;
-      if (prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
-          prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2)) {
-        t1 = fmaxf(t1, tmin);
-        t2 = fminf(t2, tmax);
-        if (!(t1 >= t2)) {
-          t1 = t1 > 0.0f ? t1 : 0.0f;
-          const float len = sqrtf(dd);
-          const float inside = (t2 - t1) * len;
-          const float dist = m.neg_inv_density * rtm::logf(g.f32());
-          if (!(dist > inside)) {
-            const float t = t1 + dist / len;
-            tmax = t;
-            h.t = t;
-            h.prim = ref;
-            h.xform = frame;
-            found = true;
-          }
+  }
+  const float4 q0 = S.pre[2 * T.p], q1 = S.pre[2 * T.p + 1];
+  const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
+  const int kind = rt_ref_kind(ref);
+  const int32_t idx = rt_ref_index(ref);
+  const f3 o = T.o, d = T.d;
+  uint32_t next = T.p + 1;
+  float t = 0.0f;
+  bool hit = false;
+  if ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) {
+    rt_bvh_node nd;
+    nd.lo[0] = q0.x, nd.lo[1] = q0.y, nd.lo[2] = q0.z;
+    nd.hi[0] = q0.w, nd.hi[1] = q1.x, nd.hi[2] = q1.y;
+    if (!aabb_hit(nd, o, T.inv, tmin, T.tmax)) next = __builtin_bit_cast(uint32_t, q1.z);
+  } else if (kind == RT_KIND_SPHERE) {  // center and r^2 inline: no dependent load
+    rt_sphere sp;
+    sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
+    hit = sphere_t(sp, o, d, T.dd, tmin, T.tmax, t);
+  } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
+    // quad_t with the plane (normal, D) inline: the quad record is read only past the plane test
+    const f3 nq = mk(q0.x, q0.y, q0.z);
+    const float denom = dot(nq, d);
+    const float tt = (q0.w - dot(nq, o)) / denom;
+    hit = !(fabsf(denom) < 1e-8f) && !((tt < tmin) || (tt > T.tmax));
+    if (hit) {
+      const rt_quad &qd = S.quads[idx];
+      const f3 hp = sub(ray_at(o, d, tt), ld3(qd.Q));
+      const f3 w = ld3(qd.w);
+      const float alpha = dot(w, cross(hp, ld3(qd.v)));
+      const float beta = dot(w, cross(ld3(qd.u), hp));
+      hit = !((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1));
+      t = tt;
+    }
+  } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
+    T.frame = ref;
+    T.fend = __builtin_bit_cast(uint32_t, q0.x);
+    T.fpos = T.p;
+    local_ray(S, T.frame, wo, wd, T.o, T.d);
+    T.inv = mk(1.0f / T.d.x, 1.0f / T.d.y, 1.0f / T.d.z);
+    T.dd = dot(T.d, T.d);
+  } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
+    // ConstantMedium_hit (src/hittable.c:392-423): two boundary hits, clamp, one rng draw
+    const rt_medium m = S.media[idx];
+    float t1, t2;
+    if (prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
+        prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2)) {
+      t1 = fmaxf(t1, tmin);
+      t2 = fminf(t2, T.tmax);
+      if (!(t1 >= t2)) {
+        t1 = t1 > 0.0f ? t1 : 0.0f;
+        const float len = sqrtf(T.dd);
+        const float inside = (t2 - t1) * len;
+        const float dist = m.neg_inv_density * rtm::logf(g.f32());
+        if (!(dist > inside)) {
+          t = t1 + dist / len;
+          hit = true;
         }
       }
     }
-    p = next;
   }
-  return found;
+  if (hit) {
+    T.tmax = t;
+    T.h.t = t;
+    T.h.prim = ref;
+    T.h.xform = T.frame;
+    T.found = true;
+  }
+  T.p = next;
+  return next >= n;
+}
+
+template <int F>
+RT_D bool trace_pre(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
+  PreTrace T;
+  pre_begin(T, wo, wd);
+  while (!pre_step<F>(S, T, wo, wd, tmin, g)) {
+  }
+  h = T.h;
+  return T.found;
 }
 
 // Host: the preorder entries of trace_pre for a flattened scene (2 float4 per entry).

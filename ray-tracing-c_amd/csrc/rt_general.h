@@ -20,9 +20,15 @@ struct GeneralView {
   int32_t *work_counter;     // zeroed before each launch
   const int32_t *order;      // work item order (longest-first), or null
   uint32_t *cost_out;        // cost pass: rays traced per work item, or null
+  int32_t batch;             // kBatch: shade once this many lanes of a wave wait (RT_GEN_BATCH)
 };
 
-template <int F>
+constexpr int kTraceSteps = 4;  // kBatch: preorder entries per lane per traversal iteration
+
+// kBatch (scenes with a preorder, S.pre): the trace runs a few entries per wave iteration
+// (pre_step) and a wave shades only once `batch` of its lanes wait -- as rt_book1.h's v3 loop --
+// instead of every lane waiting for the wave's longest trace each bounce.
+template <int F, bool kBatch = false>
 __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) {
   const DScene &S = V.S;
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
@@ -47,6 +53,9 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
   g.inc = 0;
   f3 acc = mk(0.0f, 0.0f, 0.0f), o = acc, d = acc, pixel_pos = acc;
   bool need_pixel = true, need_sample = true, done = false;
+  PreTrace T;  // kBatch: the lane's trace in progress (tracing) or finished, not yet shaded (pending)
+  T.found = false;
+  bool tracing = false, pending = false;
 
   for (;;) {
     // ---- refill (src/raytracing.c:93-94): lanes without a pixel take the next ones
@@ -76,6 +85,25 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
       }
     }
     if (__ballot(!done) == 0) break;
+    if (kBatch) {
+      const uint64_t tr = __ballot(!done && tracing);
+      const uint64_t ready = __ballot(!done && !tracing);
+      const int live = (int)__popcll(tr | ready);
+      const int batch = min(V.batch, (3 * live + 3) / 4);
+      if (tr != 0 && (int)__popcll(ready) < batch) {  // traversal steps for the lanes still tracing
+        if (tracing) {
+#pragma unroll 1
+          for (int k = 0; k < kTraceSteps; k++)
+            if (pre_step<F>(S, T, o, d, 1e-3f, g)) {
+              tracing = false;
+              pending = true;
+              break;
+            }
+        }
+        continue;
+      }
+      if (tracing) continue;  // sits out this shading pass
+    }
     if (done) continue;
     bool write = spp <= 0 && !need_pixel;  // no samples: the mean is 0/0 (src/raytracing.c:127)
     // ---- camera ray (src/raytracing.c:100-122)
@@ -107,8 +135,22 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
       path_done = true;
     } else {
       Hit h;
-      rays++;
-      if (!(S.pre ? trace_pre<F>(S, o, d, 1e-3f, g, h) : trace<F>(S, o, d, 1e-3f, g, h))) {
+      bool found;
+      if (kBatch) {
+        if (!pending) {  // start this bounce's trace; it is shaded in a later pass
+          pre_begin(T, o, d);
+          tracing = true;
+          rays++;
+          continue;
+        }
+        pending = false;
+        found = T.found;
+        h = T.h;
+      } else {
+        rays++;
+        found = S.pre ? trace_pre<F>(S, o, d, 1e-3f, g, h) : trace<F>(S, o, d, 1e-3f, g, h);
+      }
+      if (!found) {
         tail = ld3(S.cam.background);
         path_done = true;
       } else {
@@ -136,6 +178,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
           o = r.p;
           d = dir;
           depth--;
+          if (kBatch && depth > 0) {  // the next bounce's trace starts at once
+            pre_begin(T, o, d);
+            tracing = true;
+            rays++;
+          }
         }
       }
     }

@@ -189,9 +189,9 @@ __global__ void split_walk_kernel(b1::Book1View V, uint8_t *__restrict__ out, co
 }
 
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
-template <int F>
+template <int F, bool kBatch = false>
 __global__ __launch_bounds__(gen::kBlock) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
-  gen::render_general<F>(V, out);
+  gen::render_general<F, kBatch>(V, out);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -462,6 +462,7 @@ struct rt_device_scene {
   int split_rounds_used = 0;
   int sp_grid = 0;  // resident workgroups of rt_book1_split_kernel
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
+  int gen_batch = 0;          // general kernel: batched shading threshold (0: one bounce per iteration)
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1069,8 +1070,16 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0;
-  const void *fn = (d->features & ~kFeatBook1) == 0 ? (const void *)rt_general_kernel<kFeatBook1>
-                                                     : (const void *)rt_general_kernel<kFeatAll>;
+  {
+    const char *eb = getenv("RT_GEN_BATCH");
+    d->gen_batch = (eb && *eb) ? atoi(eb) : 48;
+    if (d->gen_batch < 0) d->gen_batch = 0;
+    if (d->gen_batch > 64) d->gen_batch = 64;
+    if (!d->view.pre) d->gen_batch = 0;  // the batched loop runs the preorder scan
+  }
+  const bool fb = (d->features & ~kFeatBook1) == 0;
+  const void *fn = d->gen_batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
+                                : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gen::kBlock, 0));
   if (per_cu < 1) per_cu = 1;
   d->gen_grid = prop.multiProcessorCount * per_cu;
@@ -1434,6 +1443,19 @@ static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   return 0;
 }
 
+static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, hipStream_t st, gen::GeneralView V,
+                           uint8_t *d_out) {
+  V.batch = d->gen_batch;
+  if (all && d->gen_batch)
+    hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true>), g, b, 0, st, V, d_out);
+  else if (all)
+    hipLaunchKernelGGL((rt_general_kernel<kFeatAll, false>), g, b, 0, st, V, d_out);
+  else if (d->gen_batch)
+    hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true>), g, b, 0, st, V, d_out);
+  else
+    hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, false>), g, b, 0, st, V, d_out);
+}
+
 extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out,
                                     void *stream) {
   if (!d || !d_out) return rt_set_error("rt_render_rows_async: NULL argument"), -1;
@@ -1554,9 +1576,9 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       P.cost_out = d->lpt_cost;
       HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
       if (all)
-        hipLaunchKernelGGL(rt_general_kernel<kFeatAll>, gg, gb, 0, st, P, d_out);
+        launch_general(d, true, gg, gb, st, P, d_out);
       else
-        hipLaunchKernelGGL(rt_general_kernel<kFeatBook1>, gg, gb, 0, st, P, d_out);
+        launch_general(d, false, gg, gb, st, P, d_out);
       HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
       unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
@@ -1577,9 +1599,9 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
     HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
     if (all)
-      hipLaunchKernelGGL(rt_general_kernel<kFeatAll>, gg, gb, 0, st, G, d_out);
+      launch_general(d, true, gg, gb, st, G, d_out);
     else
-      hipLaunchKernelGGL(rt_general_kernel<kFeatBook1>, gg, gb, 0, st, G, d_out);
+      launch_general(d, false, gg, gb, st, G, d_out);
     HIP_OK(hipGetLastError());
     if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
     return 0;
