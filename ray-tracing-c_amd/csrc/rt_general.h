@@ -21,9 +21,8 @@ struct GeneralView {
   const int32_t *order;      // work item order (longest-first), or null
   uint32_t *cost_out;        // cost pass: rays traced per work item, or null
   int32_t batch;             // kBatch: shade once this many lanes of a wave wait (RT_GEN_BATCH)
+  int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
 };
-
-constexpr int kTraceSteps = 4;  // kBatch: preorder entries per lane per traversal iteration
 
 // kBatch (scenes with a preorder, S.pre): the trace runs a few entries per wave iteration
 // (pre_step) and a wave shades only once `batch` of its lanes wait -- as rt_book1.h's v3 loop --
@@ -93,7 +92,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
       if (tr != 0 && (int)__popcll(ready) < batch) {  // traversal steps for the lanes still tracing
         if (tracing) {
 #pragma unroll 1
-          for (int k = 0; k < kTraceSteps; k++)
+          for (int k = 0; k < V.steps; k++)
             if (pre_step<F>(S, T, o, d, 1e-3f, g)) {
               tracing = false;
               pending = true;

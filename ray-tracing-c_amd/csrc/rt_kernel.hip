@@ -463,6 +463,7 @@ struct rt_device_scene {
   int sp_grid = 0;  // resident workgroups of rt_book1_split_kernel
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_batch = 0;          // general kernel: batched shading threshold (0: one bounce per iteration)
+  int gen_steps = 8;          // general kernel: preorder entries per traversal iteration
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1072,10 +1073,13 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   int per_cu = 0;
   {
     const char *eb = getenv("RT_GEN_BATCH");
-    d->gen_batch = (eb && *eb) ? atoi(eb) : 48;
+    d->gen_batch = (eb && *eb) ? atoi(eb) : 56;
     if (d->gen_batch < 0) d->gen_batch = 0;
     if (d->gen_batch > 64) d->gen_batch = 64;
     if (!d->view.pre) d->gen_batch = 0;  // the batched loop runs the preorder scan
+    const char *es = getenv("RT_GEN_STEPS");
+    d->gen_steps = (es && *es) ? atoi(es) : 8;
+    if (d->gen_steps < 1) d->gen_steps = 1;
   }
   const bool fb = (d->features & ~kFeatBook1) == 0;
   const void *fn = d->gen_batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
@@ -1446,6 +1450,7 @@ static int launch_split(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
 static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, hipStream_t st, gen::GeneralView V,
                            uint8_t *d_out) {
   V.batch = d->gen_batch;
+  V.steps = d->gen_steps;
   if (all && d->gen_batch)
     hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true>), g, b, 0, st, V, d_out);
   else if (all)
