@@ -403,6 +403,42 @@ __global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, 
     order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
 }
 
+// The whole-wave items (the first hist[512] of the order) exactly longest first: the buckets keep
+// an arbitrary order among items of up to 12.5 % different cost, and with a few whole waves per
+// hundred items the heaviest pixel could start only after a wave's first item (measured at N = 8:
+// started at 72 ms, the frame's last item).  One workgroup, bitonic sort of up to kCoopSort items.
+constexpr int kCoopSort = 8192;
+__global__ __launch_bounds__(1024) void lpt_coop_sort_kernel(const uint32_t *cost, const uint32_t *hist, int32_t *order) {
+  __shared__ uint32_t key[kCoopSort];
+  __shared__ int32_t val[kCoopSort];
+  const int n = (int)min(hist[512], (uint32_t)kCoopSort);
+  if (n < 2) return;
+  int m = 2;
+  while (m < n) m <<= 1;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    key[i] = i < n ? cost[order[i]] : 0u;  // padding sorts last (descending)
+    val[i] = i < n ? order[i] : -1;
+  }
+  __syncthreads();
+  for (int k = 2; k <= m; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool desc = (i & k) == 0;  // descending overall
+          const uint32_t a = key[i], b = key[l];
+          if (desc ? a < b : a > b) {
+            key[i] = b, key[l] = a;
+            const int32_t t = val[i];
+            val[i] = val[l], val[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) order[i] = val[i];
+}
+
 // ------------------------------------------------------------------------------ device scene
 struct rt_device_scene {
   int device;
@@ -939,7 +975,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s) {
     }
   }
   if (d->book1_ver == 9 && !d->book1_stats) {  // whole-wave items run concurrently on a second stream
-    HIP_OK(hipStreamCreateWithFlags(&d->wave_stream, hipStreamNonBlocking));
+    // high priority: the whole-wave workgroups take CU slots ahead of the lane / group kernel's
+    // (their chains set the frame time; measured at N = 8 their first items started at ~70 ms)
+    int prio_lo = 0, prio_hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIP_OK(hipStreamCreateWithPriority(&d->wave_stream, hipStreamNonBlocking,
+                                       env_flag("RT_WAVE_PRIO", true) ? prio_hi : prio_lo));
     HIP_OK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
   }
@@ -1514,6 +1555,8 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
       hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, coop_bucket,
                          d->coop_waves, prio_bucket, model);
       hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
+      if (d->coop_waves != 0 && d->wave_stream && env_flag("RT_COOP_SORT", true))
+        hipLaunchKernelGGL(lpt_coop_sort_kernel, dim3(1), dim3(1024), 0, st, d->lpt_cost, d->lpt_hist, d->lpt_order);
       HIP_OK(hipGetLastError());
       V.order = d->lpt_order;
       V.n_heavy = d->prio_steps > 0 ? d->lpt_hist + 514 : nullptr;

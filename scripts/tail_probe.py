@@ -47,6 +47,13 @@ for name, m in (("lane", ~coop), ("wave", coop)):
     clk = dur[m] * 2.4e6 / np.maximum(steps[m], 1)  # ~2.4 GHz shader clock per estimated step
     print(f"  {name}: items {int(m.sum())}, end p50/p90/p99/max {np.percentile(end[m], [50, 90, 99, 100]).round(1)} ms, "
           f"start max {start[m].max():.1f} ms, clocks/step p50/p90 {np.percentile(clk, [50, 90]).round(0)}")
+nc = int(ncoop[0])
+if nc:
+    head = order[: min(nc, 8)]
+    print("  whole-wave order head (item, pre-pass steps/sample, start ms, end ms):",
+          [(int(k), round(float(cost[k]) / lpt_spp), round(float(start[k]), 1), round(float(end[k]), 1)) for k in head])
+    print(f"  whole-wave start min {start[coop].min():.1f} ms; heaviest whole-wave item at order position "
+          f"{int(np.argmax(cost[order[:nc]]))}")
 last = np.argsort(-end)[:12]
 print("  last to finish: (item, mode, pre-pass steps/sample, start ms, end ms)")
 for k in last:
