@@ -190,7 +190,7 @@ __global__ void split_walk_kernel(b1::Book1View V, uint8_t *__restrict__ out, co
 
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
 template <int F, bool kBatch = false>
-__global__ __launch_bounds__(gen::kBlock) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
+__global__ __launch_bounds__(gen::kBlock, kBatch ? 3 : 1) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
   gen::render_general<F, kBatch>(V, out);
 }
 
