@@ -181,3 +181,16 @@ def test_split_render_north_star_scene(manifest, env, monkeypatch):
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
     img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"], env
+
+
+@pytest.mark.parametrize("env", [{"RT_GEN_PRE": "0"}, {"RT_GEN_BATCH": "0"}, {"RT_GEN_BATCH": "1", "RT_GEN_STEPS": "1"},
+                                 {"RT_GEN_BATCH": "64", "RT_GEN_STEPS": "32"}, {"RT_LPT": "0"}])
+@pytest.mark.parametrize("name", ["s5_200x112_16spp_d50", "s6_200x200_16spp_d50", "s7_200x200_8spp_d50"])
+def test_general_path_variants(manifest, name, env, monkeypatch):
+    """The general kernel's trace (preorder scan or stack) and loop (batched or one bounce per
+    iteration) variants must all reproduce the reference frames (transforms, media, lights)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = manifest["renders"][name]
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    _check(img, golden_image(e), f"{name} {env}")
