@@ -397,8 +397,10 @@ RT_D void pre_begin(PreTrace &T, f3 wo, f3 wd) {
   T.found = false;
 }
 // One entry of the scan; returns true once the scan is past the last entry.
+// lds / n_lds: the first n_lds entries staged in LDS by the caller (0: none)
 template <int F>
-RT_D bool pre_step(const DScene &S, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g) {
+RT_D bool pre_step(const DScene &S, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g, const float4 *lds = nullptr,
+                   uint32_t n_lds = 0u) {
   const uint32_t n = (uint32_t)S.n_pre;
   if (T.p >= n) return true;
   if (F & RT_FEAT_XFORM) {
@@ -412,7 +414,12 @@ RT_D bool pre_step(const DScene &S, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32
       T.dd = dot(T.d, T.d);
     }
   }
-  const float4 q0 = S.pre[2 * T.p], q1 = S.pre[2 * T.p + 1];
+  float4 q0, q1;
+  if (T.p < n_lds) {
+    q0 = lds[2 * T.p], q1 = lds[2 * T.p + 1];
+  } else {
+    q0 = S.pre[2 * T.p], q1 = S.pre[2 * T.p + 1];
+  }
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
   const int kind = rt_ref_kind(ref);
   const int32_t idx = rt_ref_index(ref);

@@ -22,14 +22,20 @@ struct GeneralView {
   uint32_t *cost_out;        // cost pass: rays traced per work item, or null
   int32_t batch;             // kBatch: shade once this many lanes of a wave wait (RT_GEN_BATCH)
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
+  int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
 };
 
 // kBatch (scenes with a preorder, S.pre): the trace runs a few entries per wave iteration
 // (pre_step) and a wave shades only once `batch` of its lanes wait -- as rt_book1.h's v3 loop --
 // instead of every lane waiting for the wave's longest trace each bounce.
 template <int F, bool kBatch = false>
-__device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) {
+__device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, float4 *lds = nullptr) {
   const DScene &S = V.S;
+  const uint32_t n_lds = kBatch && lds ? (uint32_t)min(V.n_lds, S.n_pre) : 0u;
+  if (n_lds) {  // the top of the preorder (the first BVH levels of every root item) in LDS
+    for (uint32_t q = threadIdx.x; q < 2 * n_lds; q += blockDim.x) lds[q] = S.pre[q];
+    __syncthreads();
+  }
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
   const int W = S.cam.width;
   const int64_t total = (int64_t)V.n_rows * W;
@@ -93,7 +99,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out) 
         if (tracing) {
 #pragma unroll 1
           for (int k = 0; k < V.steps; k++)
-            if (pre_step<F>(S, T, o, d, 1e-3f, g)) {
+            if (pre_step<F>(S, T, o, d, 1e-3f, g, lds, n_lds)) {
               tracing = false;
               pending = true;
               break;

@@ -191,7 +191,8 @@ __global__ void split_walk_kernel(b1::Book1View V, uint8_t *__restrict__ out, co
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
 template <int F, bool kBatch = false>
 __global__ __launch_bounds__(gen::kBlock, kBatch ? 3 : 1) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
-  gen::render_general<F, kBatch>(V, out);
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  gen::render_general<F, kBatch>(V, out, (float4 *)lds);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -500,6 +501,7 @@ struct rt_device_scene {
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_batch = 0;          // general kernel: batched shading threshold (0: one bounce per iteration)
   int gen_steps = 8;          // general kernel: preorder entries per traversal iteration
+  int gen_lds = 0;            // general kernel: preorder entries staged in LDS
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1118,6 +1120,11 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
     if (d->gen_batch < 0) d->gen_batch = 0;
     if (d->gen_batch > 64) d->gen_batch = 64;
     if (!d->view.pre) d->gen_batch = 0;  // the batched loop runs the preorder scan
+    const char *el = getenv("RT_GEN_LDS");
+    d->gen_lds = d->gen_batch ? ((el && *el) ? atoi(el) : 1024) : 0;
+    if (d->gen_lds < 0) d->gen_lds = 0;
+    if (d->gen_lds > d->view.n_pre) d->gen_lds = d->view.n_pre;
+    if (d->gen_lds > 2048) d->gen_lds = 2048;  // 64 KB: the default dynamic LDS limit
     const char *es = getenv("RT_GEN_STEPS");
     d->gen_steps = (es && *es) ? atoi(es) : 8;
     if (d->gen_steps < 1) d->gen_steps = 1;
@@ -1125,7 +1132,7 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const bool fb = (d->features & ~kFeatBook1) == 0;
   const void *fn = d->gen_batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
                                 : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gen::kBlock, 0));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gen::kBlock, (size_t)d->gen_lds * 2 * sizeof(float4)));
   if (per_cu < 1) per_cu = 1;
   d->gen_grid = prop.multiProcessorCount * per_cu;
   d->general = true;
@@ -1492,12 +1499,14 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
                            uint8_t *d_out) {
   V.batch = d->gen_batch;
   V.steps = d->gen_steps;
+  V.n_lds = d->gen_lds;
+  const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
   if (all && d->gen_batch)
-    hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true>), g, b, 0, st, V, d_out);
+    hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true>), g, b, lds_bytes, st, V, d_out);
   else if (all)
     hipLaunchKernelGGL((rt_general_kernel<kFeatAll, false>), g, b, 0, st, V, d_out);
   else if (d->gen_batch)
-    hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true>), g, b, 0, st, V, d_out);
+    hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true>), g, b, lds_bytes, st, V, d_out);
   else
     hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, false>), g, b, 0, st, V, d_out);
 }

@@ -184,7 +184,8 @@ def test_split_render_north_star_scene(manifest, env, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"RT_GEN_PRE": "0"}, {"RT_GEN_BATCH": "0"}, {"RT_GEN_BATCH": "1", "RT_GEN_STEPS": "1"},
-                                 {"RT_GEN_BATCH": "64", "RT_GEN_STEPS": "32"}, {"RT_LPT": "0"}])
+                                 {"RT_GEN_BATCH": "64", "RT_GEN_STEPS": "32"}, {"RT_LPT": "0"}, {"RT_GEN_LDS": "0"},
+                                 {"RT_GEN_LDS": "7"}, {"RT_GEN_LDS": "2048"}])
 @pytest.mark.parametrize("name", ["s5_200x112_16spp_d50", "s6_200x200_16spp_d50", "s7_200x200_8spp_d50"])
 def test_general_path_variants(manifest, name, env, monkeypatch):
     """The general kernel's trace (preorder scan or stack) and loop (batched or one bounce per
