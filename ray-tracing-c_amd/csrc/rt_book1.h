@@ -36,19 +36,18 @@ struct FastMat {   // 32 B: material resolved to what the Book-1 path needs
   int32_t pad[3];
 };
 
-// Split render (stream split, render_batched kMode 2).  A pixel's samples share one pcg32 stream:
-// sample s starts at stream offset o_s and draws D(o_s), so o_{s+1} = o_s + D(o_s), and a sample's
-// colour and draw count are functions of its start offset alone.  A split pixel's stream [0, len)
-// is cut into K segments at offsets B_k.  Segment 0 is the pixel's head chain (samples in order from
-// offset 0, accumulated like an unsplit pixel).  Segment k > 0 runs chains from each offset of the
-// window [B_k, B_k + w) in turn, sample after sample until the segment's end, storing each sample's
-// colour and draw count at its offset; a chain stops at an offset another chain already claimed, so
-// the window's chains coalesce.  split_walk_kernel then follows the true chain through the records
-// and adds the sample colours in sample order -- the reference's summation order, so the pixel is
-// bit-identical.  An offset the true chain needs but no chain evaluated (a draw count larger than
-// the window, or a stream longer than len) continues as a head chain in a fix-up round.
-// The records are allocated past the estimate (len > len_run): a stream longer than the chains of
-// the first round covered is split again from the walk's exact position (split_replan_kernel).
+// Split render (stream split, render_batched kMode 2; opt-in RT_SPLIT=1).  A pixel's samples share
+// one pcg32 stream: sample s starts at stream offset o_s and draws D(o_s), so o_{s+1} = o_s + D(o_s),
+// and a sample's colour and draw count are functions of its start offset alone.  A split pixel's
+// estimated stream is cut into K segments at offsets B_k.  Segment k > 0 is one chain per offset
+// of the window [B_k, B_k + w) (one lane each), sample after sample until the segment's end, each
+// storing every sample's colour and draw count at its offset; a chain stops at an offset another
+// chain already claimed, so the window's chains coalesce onto the true one.  The head chain is the
+// pixel's true chain: it computes segment 0, then takes the finished records in sample order --
+// the reference's summation order, so the pixel is bit-identical -- and computes any sample that
+// has no finished record itself (a draw count larger than the window, a stream longer than the
+// estimate, or a segment still running).  split_walk_kernel / split_replan_kernel finish any pixel
+// a round leaves unfinished (with walking heads, none).
 struct SplitPx {            // 48 B per work item of a split launch
   float acc[3];             // head chain: colour sum of samples [0, s)
   uint32_t o, s;            // head chain: next sample's start offset and index (s == spp: written)
