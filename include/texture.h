@@ -5,9 +5,10 @@
  * (rt_device.h, rt_texture_value), so calling `value` on the host aborts.
  *
  * Image textures: the reference decodes files with the (un-vendored) stb_image submodule.  This
- * library reads binary PPM (P6) directly; any other or missing file — e.g. the reference's
- * `earthmap.jpg`, which is not distributed — is replaced by the documented deterministic
- * substitute image (DESIGN.md §"Substitute earth image") with a warning on stderr.
+ * library reads binary PPM (P6) — the format is taken from the file's content, as stb_image does —
+ * and, like the reference's assert (src/texture.c:38-42), aborts on a file it cannot read.  The
+ * reference's `earthmap.jpg` is not distributed; tests and benches use the documented substitute
+ * picture written as a PPM under that name (rtc/earth.py).
  * Unlike the reference header this one has an include guard.
  */
 #ifndef RT_TEXTURE_H

@@ -55,6 +55,25 @@ def render_pixels(scene, xs, ys) -> np.ndarray:
     return out
 
 
+_workdir = None
+
+
+def ref_workdir() -> str:
+    """A directory holding the substitute earthmap.jpg (rtc/earth.py): the reference build reads it
+    from its working directory for scenes 3 and 7 (src/main.c:104, :243)."""
+    global _workdir
+    if _workdir is None:
+        import sys
+        import tempfile
+
+        sys.path.insert(0, os.path.join(os.path.dirname(ORACLE_DIR), "ray-tracing-c_amd"))
+        from rtc import earth
+
+        _workdir = tempfile.mkdtemp(prefix="rtc_ref_")
+        earth.write_substitute(_workdir)
+    return _workdir
+
+
 def ref_render(scene_id: int, width: int, spp: int, depth: int, out_path: str, fast: bool = False,
                threads: int | None = None, timeout: float | None = None) -> tuple[int, int]:
     """Run the reference build (oracle/_ref) and return (W, H); raw RGB goes to out_path."""
@@ -62,8 +81,8 @@ def ref_render(scene_id: int, width: int, spp: int, depth: int, out_path: str, f
     env = dict(os.environ)
     if threads:
         env["OMP_NUM_THREADS"] = str(threads)
-    r = subprocess.run([exe, "render", str(scene_id), str(width), str(spp), str(depth), out_path],
-                       env=env, capture_output=True, text=True, timeout=timeout, check=True)
+    r = subprocess.run([exe, "render", str(scene_id), str(width), str(spp), str(depth), os.path.abspath(out_path)],
+                       env=env, capture_output=True, text=True, timeout=timeout, check=True, cwd=ref_workdir())
     w, h = r.stdout.split()[:2]
     return int(w), int(h)
 

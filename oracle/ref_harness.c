@@ -8,8 +8,10 @@
  *   ref_render render <scene> <width> <spp> <depth> <out.rgb>   (prints "W H" on stdout)
  *   ref_render kat
  *   ref_render dump <scene>
- * Camera defaults replicate reference src/main.c:278-287.
+ * Camera defaults replicate reference src/main.c:278-287.  Scenes 3 and 7 read earthmap.jpg from the
+ * current directory, as the reference does (run from a directory holding rtc/earth.py's picture).
  */
+#define _POSIX_C_SOURCE 200809L /* access() under -std=c11 */
 #include "hittable.h"
 #include "material.h"
 #include "raytracing.h"
@@ -20,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 void scene_metal_and_lambertian(World *world, Camera *camera);
 void scene_book1_final(World *world, Camera *camera);
@@ -75,7 +78,9 @@ static void learn_kinds(void) {
   VT_MEDIUM = ConstantMedium_new(s, 1, Solid_new(vec3(0, 0, 0)))->vtable;
   TX_SOLID = (void *)Solid_new(vec3(0, 0, 0))->value;
   TX_CHECKER = (void *)Checker_new(1, m->albedo, m->albedo)->value;
-  TX_IMAGE = (void *)Image_new("x")->value;
+  /* the reference's Image_init asserts on an unreadable file (src/texture.c:38-42): learn the image
+   * kind only when the scene's picture is present (scenes 3 and 7 need it anyway) */
+  TX_IMAGE = access("earthmap.jpg", R_OK) == 0 ? (void *)Image_new("earthmap.jpg")->value : NULL;
   PCG32 g2;
   pcg32_seed(&g2, 1, 1);
   TX_PERLIN = (void *)Perlin_new(1, 1, &g2)->value;

@@ -29,8 +29,6 @@ RT_HIDDEN Vec3 rt_tex_checker_value(const Texture *self, float u, float v, Vec3 
 RT_HIDDEN Vec3 rt_tex_image_value(const Texture *self, float u, float v, Vec3 p);
 RT_HIDDEN Vec3 rt_tex_perlin_value(const Texture *self, float u, float v, Vec3 p);
 
-/* deterministic substitute for image files this library cannot decode */
-RT_HIDDEN uint8_t *rt_substitute_image(int *width, int *height);
 
 /* reference driver scenes (src/main.c:9-273); defined in rt_scenes.c */
 void scene_metal_and_lambertian(World *world, Camera *camera);

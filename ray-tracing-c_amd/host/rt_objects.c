@@ -455,24 +455,6 @@ Texture *Checker_new(float scale, Texture *even, Texture *odd) {
   return &t->texture;
 }
 
-/* Substitute image (documented in DESIGN.md; the oracle's reference build uses the same
- * generator): 1024 x 512 RGB8, smooth ramps plus an xor pattern so every texel differs from its
- * neighbours in at least one channel. */
-uint8_t *rt_substitute_image(int *width, int *height) {
-  const int w = 1024, h = 512;
-  uint8_t *px = my_malloc((size_t)w * h * 3);
-  for (int j = 0; j < h; j++)
-    for (int i = 0; i < w; i++) {
-      uint8_t *q = px + ((size_t)j * w + i) * 3;
-      q[0] = (uint8_t)((i * 255) / (w - 1));
-      q[1] = (uint8_t)((j * 255) / (h - 1));
-      q[2] = (uint8_t)((i ^ j) & 255);
-    }
-  *width = w;
-  *height = h;
-  return px;
-}
-
 /* Binary PPM (P6, maxval 255) reader; returns NULL if the file is absent or not P6. */
 static uint8_t *read_ppm(const char *path, int *width, int *height) {
   FILE *f = fopen(path, "rb");
@@ -499,10 +481,9 @@ static uint8_t *read_ppm(const char *path, int *width, int *height) {
 void Image_init(Image *self, char *filename) {
   self->texture.value = rt_tex_image_value;
   self->buffer = read_ppm(filename, &self->width, &self->height);
-  if (self->buffer == NULL) {
-    fprintf(stderr, "rt: Image_new(\"%s\"): cannot decode (only binary PPM is read); using the substitute image\n",
-            filename);
-    self->buffer = rt_substitute_image(&self->width, &self->height);
+  if (self->buffer == NULL) {  /* the reference asserts here (src/texture.c:38-42) */
+    fprintf(stderr, "rt: Image_new(\"%s\"): Unable to read image (this library decodes binary PPM only)\n", filename);
+    abort();
   }
 }
 Texture *Image_new(char *filename) {

@@ -16,6 +16,8 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64
 
 import numpy as np
 
+from . import earth
+
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # ray-tracing-c_amd/
 LIB_PATH = os.path.join(PKG_DIR, "librtc_amd.so")
 
@@ -72,6 +74,18 @@ assert RtFlatScene.n_image_bytes.offset == 192
 
 
 _lib = None
+_subst_dir = None
+
+
+def substitute_dir() -> str:
+    """A private directory holding the substitute earthmap.jpg (created once per process)."""
+    global _subst_dir
+    if _subst_dir is None:
+        import tempfile
+
+        _subst_dir = tempfile.mkdtemp(prefix="rtc_earth_")
+        earth.write_substitute(_subst_dir)
+    return _subst_dir
 
 
 def _init_torch_runtime_first() -> None:
@@ -143,7 +157,18 @@ class Scene:
     @classmethod
     def preset(cls, scene_id: int, width: int = 0, spp: int = 0, max_depth: int = 0) -> "Scene":
         """Reference driver scene `scene_id` (0-7) with the reference defaults (500 px, 100 spp,
-        depth 50) unless overridden; aspect ratio comes from the scene (src/main.c)."""
+        depth 50) unless overridden; aspect ratio comes from the scene (src/main.c).
+
+        Scenes 3 and 7 read ``earthmap.jpg`` from the current directory, as the reference does; when
+        it is absent the preset is built in a directory holding the documented substitute picture
+        (rtc/earth.py) -- the explicit opt-in for tests and benches."""
+        if int(scene_id) in (3, 7) and not os.path.exists(earth.FILE_NAME):
+            cwd = os.getcwd()
+            os.chdir(substitute_dir())
+            try:
+                return cls(lib().rt_scene_preset(int(scene_id), int(width), int(spp), int(max_depth)))
+            finally:
+                os.chdir(cwd)
         return cls(lib().rt_scene_preset(int(scene_id), int(width), int(spp), int(max_depth)))
 
     @property

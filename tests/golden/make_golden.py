@@ -11,7 +11,8 @@ Writes (all small, all data):
   render_<cfg>.rgb.gz     full reference renders for small configs (raw RGB rows, top to bottom)
   manifest.json           every render: scene/size/spp/depth, sha256 of the full RGB buffer, crops
 
-Usage: python tests/golden/make_golden.py [--big]   (--big adds the 1200x675x1000spp frame, ~8 min)
+Usage: python tests/golden/make_golden.py [--big | --only NAME]   (--big adds the full-size frames of configs
+       3/4 (1200x675x1000spp, ~8 min) and 5 (scene 7 1000x1000x1000spp, ~35 min))
 """
 import argparse
 import gzip
@@ -25,6 +26,12 @@ import tempfile
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = os.path.join(ROOT, "oracle", "_ref", "ref_render")
+sys.path.insert(0, os.path.join(ROOT, "ray-tracing-c_amd"))
+from rtc import earth  # noqa: E402  (the documented substitute earth picture)
+
+# the reference reads earthmap.jpg from its working directory (src/main.c:104, :243)
+WORKDIR = tempfile.mkdtemp(prefix="rtc_golden_")
+earth.write_substitute(WORKDIR)
 
 # (name, scene, width, spp, depth, keep_full_image)
 SMALL = [
@@ -40,7 +47,8 @@ SMALL = [
     ("s7_200x200_8spp_d50", 7, 200, 8, 50, True),
     ("s7_400x400_16spp_d50", 7, 400, 16, 50, False),
 ]
-BIG = [("s1_1200x675_1000spp_d50", 1, 1200, 1000, 50, False)]  # the north-star frame
+BIG = [("s1_1200x675_1000spp_d50", 1, 1200, 1000, 50, False),  # the north-star frame (config 3/4)
+       ("s7_1000x1000_1000spp_d50", 7, 1000, 1000, 50, False)]  # config 5 at full size (~35 min, 8 cores)
 
 
 def crops(img, w, h, n=8, size=32):
@@ -59,7 +67,7 @@ def render(name, scene, width, spp, depth, keep, manifest):
     with tempfile.TemporaryDirectory() as td:
         raw = os.path.join(td, "out.rgb")
         r = subprocess.run([REF, "render", str(scene), str(width), str(spp), str(depth), raw],
-                           capture_output=True, text=True, check=True)
+                           capture_output=True, text=True, check=True, cwd=WORKDIR)
         w, h = map(int, r.stdout.split()[:2])
         img = open(raw, "rb").read()
     assert len(img) == w * h * 3
@@ -83,18 +91,20 @@ def main():
         sys.exit("oracle/_ref/ref_render missing: run `make -C oracle` where /root/reference exists")
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {"renders": {}}
-    manifest["generator"] = ("oracle/_ref/ref_render: reference sources built with gcc -std=c11 -O2 -fopenmp "
-                             "(glibc 2.35 libm, FMA ifuncs); texture.c restated in oracle/ref_texture.c")
+    manifest["generator"] = ("oracle/_ref/ref_render: the reference's own src/*.c (all nine files, compiled where "
+                             "they lie) built with gcc -std=c11 -O2 -fopenmp (glibc 2.35 libm, FMA ifuncs); "
+                             "stb_image (un-vendored submodule) restated in oracle/stb/stb_image.h (stbi_load, PNM "
+                             "path); scenes 3/7 read the substitute earth picture rtc/earth.py writes as earthmap.jpg")
     if not args.only:
-        kat = subprocess.run([REF, "kat"], capture_output=True, text=True, check=True).stdout
+        kat = subprocess.run([REF, "kat"], capture_output=True, text=True, check=True, cwd=WORKDIR).stdout
         open(os.path.join(HERE, "kat.txt"), "w").write(kat)
         for s in range(8):
-            d = subprocess.run([REF, "dump", str(s)], capture_output=True, text=True, check=True).stdout
+            d = subprocess.run([REF, "dump", str(s)], capture_output=True, text=True, check=True, cwd=WORKDIR).stdout
             with gzip.open(os.path.join(HERE, f"scene{s}.dump.gz"), "wt", compresslevel=9) as f:
                 f.write(d)
         with tempfile.TemporaryDirectory() as td:
             t = os.path.join(td, "x.tiff")
-            subprocess.run([REF, "render", "0", "400", "1", "1", t], capture_output=True, check=True)
+            subprocess.run([REF, "render", "0", "400", "1", "1", t], capture_output=True, check=True, cwd=WORKDIR)
             data = open(t, "rb").read()
             open(os.path.join(HERE, "tiff_header.bin"), "wb").write(data[:168])
             manifest["tiff_s0_400x225_1spp_d1"] = {"size": len(data), "sha256": hashlib.sha256(data).hexdigest()}

@@ -29,7 +29,7 @@ def test_kernel_code_on_host_matches_oracle(tmp_path, scene, width, spp, depth, 
     out = str(tmp_path / "k.rgb")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", OMP_NUM_THREADS="8")
     r = subprocess.run([EXE, str(scene), str(width), str(spp), str(depth), out, variant], capture_output=True,
-                       text=True, env=env, timeout=600)
+                       text=True, env=env, timeout=600, cwd=rtc.substitute_dir())
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.split()[2] == (variant if scene > 1 or variant in ("all", "pre") else "book1")
     sc = rtc.Scene.preset(scene, width, spp, depth)
