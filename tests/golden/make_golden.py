@@ -100,8 +100,9 @@ def main():
         open(os.path.join(HERE, "kat.txt"), "w").write(kat)
         for s in range(8):
             d = subprocess.run([REF, "dump", str(s)], capture_output=True, text=True, check=True, cwd=WORKDIR).stdout
-            with gzip.open(os.path.join(HERE, f"scene{s}.dump.gz"), "wt", compresslevel=9) as f:
-                f.write(d)
+            with open(os.path.join(HERE, f"scene{s}.dump.gz"), "wb") as raw_f, \
+                    gzip.GzipFile(fileobj=raw_f, mode="wb", compresslevel=9, mtime=0) as f:
+                f.write(d.encode())
         with tempfile.TemporaryDirectory() as td:
             t = os.path.join(td, "x.tiff")
             subprocess.run([REF, "render", "0", "400", "1", "1", t], capture_output=True, check=True, cwd=WORKDIR)
