@@ -44,15 +44,19 @@ void rt_scene_release(rt_device_scene *dscene);
 
 /* Render rows row0, row0 + row_stride, ... (n_rows of them) into d_out (device pointer,
  * n_rows * width * 3 bytes, compact, in that row order).  Asynchronous on `stream`
- * (hipStream_t, NULL = default stream of the scene's device).  This is the hot path.
- * Book-1 scenes at >= 32 spp first run a low-spp cost pass (RT_LPT_SPP, default 8; RT_LPT=0 turns
- * it off) and hand out the pixels longest-first; the image does not depend on the order. */
+ * (hipStream_t, NULL = default stream of the scene's device): no host synchronisation.  This is
+ * the hot path.  Book-1 scenes at >= 32 spp first run a low-spp cost pass (RT_LPT_SPP, default 8)
+ * that plans the launch (longest-first order; split pixel streams, rt_book1.h: ChainPx); the image
+ * does not depend on the plan.  Launches on one scene share its scratch, so each launch first waits
+ * (on the device, hipStreamWaitEvent) for the scene's previous launch, on whatever stream that was;
+ * launches on different scenes are independent. */
 int rt_render_rows_async(rt_device_scene *dscene, int row0, int row_stride, int n_rows, uint8_t *d_out,
                          void *stream);
 
 /* Whole frame into a host buffer (width*height*3), rows interleaved j mod n_gpus over GPUs
- * 0..n_gpus-1 (n_gpus <= 0: all visible), one host thread + stream per GPU, no collectives.
- * Synchronous.  This is what Camera_render calls. */
+ * 0..n_gpus-1 (n_gpus <= 0: all visible), no collectives.  The host-side preprocessing of the scene
+ * runs once; then one host thread per GPU uploads, launches on its own stream and copies its rows
+ * back.  Synchronous.  This is what Camera_render calls. */
 int rt_render(const rt_flat_scene *scene, int n_gpus, uint8_t *out_host);
 
 /* Kernel-side timing of the last rt_render call on `device`: milliseconds between HIP events
@@ -64,17 +68,6 @@ double rt_last_kernel_ms(int device);
  *     4 = atan2f(x[2i], x[2i+1]) into out[i] (n = 2 * pairs), 5 = acosf. */
 int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device);
 
-/* Diagnostics: counters of the last Book-1 launch built with RT_BOOK1_STATS=1 set at upload time
- * (first n of: trav iterations, useful steps, shade iterations, shading lanes, rays, node visits,
- * root-leaf steps, idle-in-shade iterations, shader clocks in traversal / shading iterations,
- * wave-level traversal / shading iterations, v6 wave-level box / sphere phases or v5 fast / fallback sphere tests, v5 wave-level sphere-code
- * and fallback executions, clock64 / wall_clock64 ticks of the waves' lifetimes, earliest start / latest end,
- * latest start, first pixel-counter exhaustion (wall_clock64), v5 box hits, cooperative traces and their clocks, v9 cooperative windows and scan steps, and their window / walk clocks; n <= 29). */
-int rt_book1_stats(rt_device_scene *dscene, unsigned long long *out, int n);
-/* Diagnostics (same stats build): per work item of the last launch, {traversal steps, duration in
- * wall_clock64 ticks (100 MHz)} as 2 x uint32 each, for the first n_items items. */
-int rt_book1_pixel_cost(rt_device_scene *dscene, uint32_t *out, int64_t n_items);
-
 /* Diagnostics: bitwise checks of the Book-1 kernel's exact arithmetic cores against the compiler's
  * sqrtf / division on the device (fn 0: sqrt over float bit patterns start..start+count-1,
  * fn 1: division on `count` hashed pairs, fn 2: the sphere-hit outcome on hashed rays);
@@ -82,8 +75,8 @@ int rt_book1_pixel_cost(rt_device_scene *dscene, uint32_t *out, int64_t n_items)
 int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigned long long *mismatches, int device);
 
 /* Milliseconds of the last frame launch rt_render_rows_async made for `dscene` (HIP events on its
- * stream; call after that work completed).  Excludes the longest-first cost pre-pass
- * (rt_book1_cost_kernel, RT_LPT).  -1 when unavailable. */
+ * stream; call after that work completed).  Excludes the cost pre-pass and the plan
+ * (rt_book1_cost_kernel, chain_* planner kernels).  -1 when unavailable. */
 double rt_scene_last_launch_ms(rt_device_scene *dscene);
 
 /* Diagnostics (RT_PX_TIME=1 set at upload time, Book-1 path): for the first n work items of the
@@ -93,7 +86,14 @@ double rt_scene_last_launch_ms(rt_device_scene *dscene);
 int rt_scene_px_time(rt_device_scene *dscene, uint32_t *times, uint32_t *cost, int32_t *order, uint32_t *n_coop,
                      int64_t n);
 
-/* Name of the kernel rt_render_rows_async launches for `dscene` (as rocprofv3 lists it). */
+/* Diagnostics (RT_PX_TIME=1 set at upload time): the last chain launch, one row of 8 uint32 per work
+ * item in item order: pixel, segment, K, whole-wave (1) / lane (0), start, end (wall_clock64 ticks,
+ * 100 MHz, low 32 bits), records written (samples for segment 0 / unsplit), flags (bit 0 coupled,
+ * bit 1 ended).  Returns the number of items (at most max_rows rows are written), -1 on error. */
+int64_t rt_scene_chain_diag(rt_device_scene *dscene, uint32_t *rows, int64_t max_rows);
+
+/* Name of the frame kernel rt_render_rows_async launches for `dscene` over its whole image (as
+ * rocprofv3 lists it). */
 const char *rt_scene_kernel(const rt_device_scene *dscene);
 
 const char *rt_last_error(void);

@@ -234,8 +234,6 @@ __device__ void render_groups(const b1::Book1View &V, uint8_t *__restrict__ out,
         L.tmax = __builtin_inff();
         L.hit = -1;
         L.cur = 0;
-        L.sp = L.k = 0;
-        L.pend0 = L.pend1 = 0xffffu;
         if (V.n_items9 > 0)
           while (!b1::trav_step_v9(V, items, L, tmin)) {
           }

@@ -1,0 +1,52 @@
+"""Timeline of one chain launch (RT_PX_TIME=1 diagnostic): every work item's start / end, by kind
+(unsplit lane pixel, lane segment, whole-wave segment), and the items that finish last.
+    python scripts/chain_probe.py WORLD RANK [SPP]       (RT_* knobs from the environment)"""
+import ctypes
+import os
+import sys
+import time
+
+os.environ["RT_PX_TIME"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ray-tracing-c_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import rtc  # noqa: E402
+
+world, rank = int(sys.argv[1]), int(sys.argv[2])
+spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+sc = rtc.Scene.preset(1, 1200, spp, 50)
+ds = rtc.DeviceScene(sc, 0)
+row0, stride, n = rtc.rows_of(sc.height, rank, world)
+buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream()
+for _ in range(2):
+    t0 = time.perf_counter()
+    ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+L = rtc.lib()
+L.rt_scene_chain_diag.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+L.rt_scene_chain_diag.restype = ctypes.c_int64
+cap = sc.width * sc.height * 64
+rows = np.zeros((cap, 8), np.uint32)
+m = L.rt_scene_chain_diag(ds._h, rows.ctypes.data, cap)
+assert m >= 0, rtc.last_error()
+r = rows[:m].astype(np.int64)
+t0 = r[:, 4].min()
+start = (r[:, 4] - t0) / 1e5  # wall_clock64: 100 MHz -> ms
+end = (r[:, 5] - t0) / 1e5
+print(f"world={world} rank={rank} ms={t * 1e3:.1f} kernel_ms={ds.last_launch_ms():.1f} items={m} "
+      f"last_end={end.max():.1f} ms", flush=True)
+kinds = {"unsplit lane": (r[:, 2] == 1) & (r[:, 3] == 0), "unsplit wave": (r[:, 2] == 1) & (r[:, 3] == 1),
+         "segment lane": (r[:, 2] > 1) & (r[:, 3] == 0), "segment wave": (r[:, 2] > 1) & (r[:, 3] == 1)}
+for name, k in kinds.items():
+    if k.any():
+        d = end[k] - start[k]
+        print(f"  {name:13s} items {k.sum():7d}  end p50/p90/p99/max {np.percentile(end[k], [50, 90, 99, 100]).round(1)} ms"
+              f"  start max {start[k].max():.1f}  duration p50/p99/max {np.percentile(d, [50, 99, 100]).round(1)}"
+              f"  records p50/max {np.percentile(r[k, 6], [50, 100])}", flush=True)
+last = np.argsort(-end)[:16]
+print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, flags)")
+for q in last:
+    print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]}")
+ds.close()

@@ -139,19 +139,27 @@ def test_cli_rt_main_matches_golden(manifest, tmp_path):
     assert data[:168] == open(os.path.join(ROOT, "tests", "golden", "tiff_header.bin"), "rb").read()
 
 
-@pytest.mark.parametrize("env", [{"RT_BOOK1": "0"}, {"RT_BOOK1": "0", "RT_GENERAL": "0"}, {"RT_BOOK1_LDS": "0"}, {}, {"RT_BOOK1_V": "2"},
-                                 {"RT_BOOK1_V": "3"}, {"RT_BOOK1_V": "5"}, {"RT_BOOK1_V": "6"}, {"RT_BOOK1_V": "7"}, {"RT_BOOK1_V": "9"}, {"RT_BOOK1_V": "9", "RT_BOOK1_LDS": "0"}, {"RT_BOOK1_V": "9", "RT_COOP_LANES": "64"}, {"RT_BOOK1_V": "5", "RT_COOP_LANES": "64"}, {"RT_BOOK1_STATS": "1"}, {"RT_LPT": "0"}, {"RT_LPT_SPP": "1"}, {"RT_COOP_STEPS": "50"}, {"RT_COOP_WAVES": "0"},
-                                 {"RT_MODE": "lane"}, {"RT_MODE": "group"}, {"RT_MODE": "group", "RT_BOOK1_LDS": "0"},
-                                 {"RT_MODE": "group", "RT_LPT": "0"}, {"RT_MODE": "lane", "RT_LPT_SPP": "1"},
-                                 {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024"},
-                                 {"RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024", "RT_BF": "0"}, {"RT_COOP_LANES": "64"}, {"RT_COOP_LANES": "0"}, {"RT_SHADE_BATCH": "1"},
-                                 {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"},
-                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1"},
-                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001"},
-                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001", "RT_SPLIT_W": "0.2"},
-                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "1", "RT_SPLIT_BETA": "0.001", "RT_SPLIT_W": "0.2",
-                                  "RT_SPLIT_MARGIN": "1.0", "RT_SPLIT_ROUNDS": "1"},
-                                 {"RT_SPLIT": "1", "RT_LPT_SPP": "2", "RT_SPLIT_BETA": "0.01", "RT_SPLIT_KMAX": "3"}])
+CHAIN = {"RT_MODE": "chain", "RT_LPT_SPP": "1", "RT_CHAIN_MIN_SEG": "4"}
+
+
+@pytest.mark.parametrize("env", [
+    {}, {"RT_BOOK1": "0"}, {"RT_BOOK1": "0", "RT_GENERAL": "0"}, {"RT_BOOK1_LDS": "0"},
+    {"RT_MODE": "lane"}, {"RT_MODE": "lane", "RT_LPT": "0"}, {"RT_MODE": "lane", "RT_LPT_SPP": "1"},
+    {"RT_MODE": "lane", "RT_COOP_STEPS": "50"}, {"RT_MODE": "lane", "RT_COOP_WAVES": "0"},
+    {"RT_MODE": "lane", "RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024"},
+    {"RT_MODE": "lane", "RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024", "RT_BF": "0"},
+    {"RT_MODE": "lane", "RT_BOOK1_LDS": "0", "RT_LPT_SPP": "1"},
+    {"RT_MODE": "group"}, {"RT_MODE": "group", "RT_BOOK1_LDS": "0"}, {"RT_MODE": "group", "RT_LPT": "0"},
+    {"RT_SHADE_BATCH": "1"}, {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"},
+    CHAIN,                                                         # the chain render, planned
+    {**CHAIN, "RT_CHAIN_BETA": "0.001"},                           # every pixel split as far as allowed
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_KMAX": "64"},    # many short segments (lanes)
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_KMAX": "1"},     # every split pixel on whole waves
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},  # continuations
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_MB": "1"},       # out of records: pixels stay whole
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BOOK1_LDS": "0"},      # global-memory scene, lanes only
+    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BF": "0", "RT_CHAIN_KMAX": "2"},
+])
 @pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
 def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
     """Book-1 scenes run on the persistent fast kernel (LDS or global geometry) unless RT_BOOK1=0
@@ -169,13 +177,15 @@ def test_book1_deep_paths_spill(monkeypatch):
     _check(rtc.render(sc), pyoracle.render(sc), "scene 1 depth 64")
 
 
-@pytest.mark.parametrize("env", [{}, {"RT_SPLIT_BETA": "0.002"}, {"RT_SPLIT_BETA": "0.002", "RT_SPLIT_W": "0.2", "RT_SPLIT_MARGIN": "1.0"}])
-def test_split_render_north_star_scene(manifest, env, monkeypatch):
-    """Stream-split render (rt_book1.h: SplitPx) forced on the Book-1 final scene at full size: pixels
-    cut into segments of their pcg32 stream, windows of speculative chains, the walk and the fix-up
-    rounds must reproduce the reference frame bit for bit."""
-    monkeypatch.setenv("RT_SPLIT", "1")
+@pytest.mark.parametrize("env", [{}, {"RT_CHAIN_BETA": "0.002"}, {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_KMAX": "64"},
+                                 {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"}])
+def test_chain_render_north_star_scene(manifest, env, monkeypatch):
+    """Chain render (rt_book1.h: ChainPx) forced on the Book-1 final scene at full size: pixel
+    streams cut into segments, chains coupling on equal stream offsets, the fold and the
+    continuations must reproduce the reference frame bit for bit."""
+    monkeypatch.setenv("RT_MODE", "chain")
     monkeypatch.setenv("RT_LPT_SPP", "2")
+    monkeypatch.setenv("RT_CHAIN_MIN_SEG", "2")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
