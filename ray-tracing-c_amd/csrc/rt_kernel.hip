@@ -1704,7 +1704,8 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   std::vector<uint2> items(n_items);
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg(n_seg);
-  std::vector<uint32_t> pt(2 * npix), sgt(2 * n_seg);
+  std::vector<uint32_t> pt(2 * npix), sgt(2 * n_seg), draws(npix);
+  HIP_OK(hipMemcpy(draws.data(), d->draw_out, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(items.data(), d->ch_items, n_items * sizeof(uint2), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(px.data(), d->ch_px, npix * sizeof(b1::ChainPx), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(seg.data(), d->ch_seg, n_seg * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1713,9 +1714,11 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   const uint32_t spp = (uint32_t)d->view.cam.spp;
   for (size_t k = 0; k < n_items && (int64_t)k < max_rows; k++) {
     const uint32_t p = items[k].x, sg = items[k].y;
-    uint32_t *r = rows + 8 * k;
+    uint32_t *r = rows + 12 * k;
     r[0] = p;
     r[3] = k < c[kCnNCoop] ? 1u : 0u;
+    r[8] = r[9] = r[10] = 0u;
+    r[11] = draws[p];
     if (sg & b1::kItemUnsplit) {
       r[1] = 0, r[2] = 1, r[4] = pt[2 * p], r[5] = pt[2 * p + 1], r[6] = spp, r[7] = 2u;
     } else {
@@ -1726,6 +1729,7 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
       r[5] = P.end0 + sg < n_seg ? sgt[2 * (P.end0 + sg) + 1] : 0u;
       r[6] = b1::end_n(w);
       r[7] = ((w & b1::kEndEnded) && !(w & b1::kEndNoLink) ? 1u : 0u) | ((w & b1::kEndEnded) ? 2u : 0u);
+      r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len;
     }
   }
   return (int64_t)n_items;

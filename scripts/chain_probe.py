@@ -28,7 +28,7 @@ L = rtc.lib()
 L.rt_scene_chain_diag.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
 L.rt_scene_chain_diag.restype = ctypes.c_int64
 cap = sc.width * sc.height * 64
-rows = np.zeros((cap, 8), np.uint32)
+rows = np.zeros((cap, 12), np.uint32)
 m = L.rt_scene_chain_diag(ds._h, rows.ctypes.data, cap)
 assert m >= 0, rtc.last_error()
 r = rows[:m].astype(np.int64)
@@ -45,8 +45,28 @@ for name, k in kinds.items():
         print(f"  {name:13s} items {k.sum():7d}  end p50/p90/p99/max {np.percentile(end[k], [50, 90, 99, 100]).round(1)} ms"
               f"  start max {start[k].max():.1f}  duration p50/p99/max {np.percentile(d, [50, 99, 100]).round(1)}"
               f"  records p50/max {np.percentile(r[k, 6], [50, 100])}", flush=True)
+# coupling: per split pixel, samples computed (head samples + every record) against spp
+sp = r[:, 2] > 1
+if sp.any():
+    pix = r[sp, 0]
+    tot = np.bincount(pix, weights=r[sp, 6])
+    Kp = np.zeros_like(tot); Kp[pix] = r[sp, 2]
+    has = Kp > 0
+    infl = tot[has] / spp
+    print(f"  split pixels {has.sum()}: samples/spp p50/p90/p99/max {np.percentile(infl, [50, 90, 99, 100]).round(3)}", flush=True)
+    mid = sp & (r[:, 1] + 1 < r[:, 2])
+    nc = mid & ((r[:, 7] & 1) == 0)
+    print(f"  non-last segments {mid.sum()}: not coupled {nc.sum()}  (records p50/max of those "
+          f"{np.percentile(r[nc, 6], [50, 100]) if nc.any() else '-'})", flush=True)
+    cpl = sp & ((r[:, 7] & 1) == 1) & (r[:, 8] > 0)
+    print(f"  link record (successor's garbage samples) p50/p90/p99/max {np.percentile(r[cpl, 9], [50, 90, 99, 100])}", flush=True)
+    lastseg = sp & (r[:, 1] + 1 == r[:, 2])
+    ratio = r[lastseg, 6] / (spp / r[lastseg, 2])
+    print(f"  last segments: records / (spp/K) p50/p90/p99/max {np.percentile(ratio, [50, 90, 99, 100]).round(2)}", flush=True)
+    est = r[sp, 10].astype(np.float64) * r[sp, 2]
+    print(f"  planned stream (seg_len*K) / (pre-pass draws * spp/8) p50 {np.median(est / np.maximum(1, r[sp, 11] * spp / 8)):.2f}", flush=True)
 last = np.argsort(-end)[:16]
-print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, flags)")
+print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, flags, link t:c, seg_len, pre-pass draws)")
 for q in last:
-    print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]}")
+    print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]} {r[q, 8]}:{r[q, 9]} {r[q, 10]} {r[q, 11]}")
 ds.close()
