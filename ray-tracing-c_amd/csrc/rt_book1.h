@@ -73,6 +73,29 @@ struct ChainCont {     // 32 B: a continuation item -- the true chain from an ex
   uint32_t pix, o, s, pad;
   float acc[4];
 };
+// Migration (tail of a launch): a lane whose wave has run out of work items and has few live lanes
+// left hands its item over at a sample boundary -- the whole state there is (pcg32 state and offset,
+// samples / records so far, colour sum, coupling cursor) -- to a wave whose lanes have all finished,
+// which runs it on to the end with whole-wave traces (render_item_coop).
+// Control words at V.mig (uint32): [0] done: the launch's finished items; [1] helpers: waves that
+// have become helpers; then kMigBoxes mailboxes of one 128-B line each:
+//   push / pop: indices into the mailbox's part of the queue; credits: its idle helpers not yet
+//   claimed by a push (a lane pushes only against a credit, so a queued item always has a helper);
+//   finished: set once every item is done (the helpers' exit).
+// Helpers poll only their own mailbox's line, rarely: thousands of idle waves polling one address
+// would swamp that memory channel and slow every working lane (measured: +30 % at N = 8).
+constexpr int kMigBoxes = 64, kMigBoxWords = 32;
+enum : int { kMigDone = 0, kMigHelpers = 1, kMigBox0 = 32, kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3 };
+constexpr int kMigWords = kMigBox0 + kMigBoxes * kMigBoxWords;
+constexpr int kMigMode = 2;  // the launches that migrate: chain launches (kMode 2)
+struct MigRec {       // 64 B
+  uint64_t state;     // pcg32 state at the sample boundary (inc follows from the pixel's seed)
+  uint32_t n;         // stream offset
+  uint32_t pix, seg, s, tc, st;
+  float acc[3];
+  uint32_t ready;     // the launch's epoch, written last (release); the helper's acquire load waits for it
+  uint32_t pad[2];
+};
 constexpr uint32_t kItemUnsplit = 0x80000000u;  // ch_items[].y: K == 1, the whole pixel
 constexpr uint64_t kEndEnded = 1ull << 63;      // end word: the segment's chain has ended
 constexpr uint64_t kEndNoLink = 1ull << 62;     //   ... without coupling (pixel complete / list full)
@@ -124,6 +147,18 @@ struct Book1View {
   uint32_t *seg_time;        // diagnostic (RT_PX_TIME=1): per segment {start, end} at end0 + k
   const ChainCont *ch_cont;  // continuation launch: items from here (else null)
   const uint32_t *ch_n_cont;
+  // migration (MigRec): control words, queue, its capacity; mig_live: a wave with at most this many
+  // live lanes (and no work items left) migrates them; 0: off
+  uint32_t *mig;
+  MigRec *mig_q;
+  uint32_t mig_cap;
+  int32_t mig_live;
+  uint32_t mig_epoch;  // per launch (> 0): marks the queue entries this launch wrote
+  int32_t mig_idle;    // migrate only once more waves than this have become helpers
+  int32_t mig_sleep;     // helpers poll their mailbox every mig_sleep * ~3.4 us
+  int32_t mig_max_help;  // at most this many finished waves stay as helpers; the others leave.  Resident
+                         // idle waves slow the working ones (measured: all 5120 waves of a grid kept
+                         // resident made N = 8 shares 20 % slower, however rarely they polled)
 };
 
 // ---------------------------------------------------------------- pixel output
@@ -644,7 +679,7 @@ RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, 
 // (kMode 2: segment / unsplit pixel, with the same boundary protocol as a lane).
 template <int kMode>
 RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix, uint32_t seg,
-                           uint8_t *__restrict__ out) {
+                           uint8_t *__restrict__ out, const MigRec *res = nullptr) {
   const rt_camera &cam = V.S.cam;
   const int W = cam.width;
   const int jj = (int)(pix / W);
@@ -657,14 +692,19 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
   g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
   f3 acc = mk(0.0f, 0.0f, 0.0f);
   uint32_t s = 0, tc = kNoTarget, st = 0;
-  if (kMode == 2 && !(seg & kItemUnsplit)) {
+  if (res) {  // a migrated item: on from the lane's sample boundary
+    g.state = res->state;
+    g.n = res->n;
+    s = res->s, tc = res->tc, st = res->st;
+    acc = mk(res->acc[0], res->acc[1], res->acc[2]);
+  } else if (kMode == 2 && !(seg & kItemUnsplit)) {
     const ChainPx &P = V.ch_px[pix];
     g.skip(seg * P.seg_len);
     if (seg + 1u < P.K) tc = (seg + 1u) << 24, st = (seg + 1u) * P.seg_len;
   }
   const bool use_bf = V.n_bf_leaves > 0;
-  const uint32_t px_start = V.px_time ? (uint32_t)wall_clock64() : 0u;
-  if (kMode == 2 && V.px_time && lane0) chain_time(V, pix, seg, 0);
+  const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
+  if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
   for (;;) {
     if (kMode == 2) {  // (wave-uniform: every lane loads the same words; lane 0's view decides)
       const bool done = chain_boundary(V, pix, seg, g.n, s, acc, tc, st, out, lane0);
@@ -752,7 +792,92 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     s++;
   }
   if (kMode != 2 && lane0) write_pixel(out + pix * 3, acc, cam.spp);
-  if (V.px_time && lane0 && kMode != 2) V.px_time[2 * pix] = px_start, V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+  if (V.px_time && lane0 && kMode != 2) {
+    if (!res) V.px_time[2 * pix] = px_start;
+    V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+  }
+}
+
+// ---------------------------------------------------------------- migration (MigRec)
+RT_D uint32_t *mig_box(const Book1View &V, uint32_t m) { return V.mig + kMigBox0 + m * kMigBoxWords; }
+
+// An item finished (in a lane or a helper): the last one tells every mailbox.
+RT_D void mig_item_done(const Book1View &V, int64_t total_own) {
+  if ((int64_t)atomicAdd(&V.mig[kMigDone], 1u) + 1 == total_own)
+    for (int m = 0; m < kMigBoxes; m++) st_rel(mig_box(V, (uint32_t)m) + kMigFinished, 1u);
+}
+
+RT_D bool mig_push(const Book1View &V, uint32_t m, int32_t pix, uint32_t seg, uint32_t s, f3 acc, const Pcg32 &g,
+                   uint32_t tc, uint32_t st) {
+  uint32_t *box = mig_box(V, m);
+  if ((int32_t)atomicSub(box + kMigCredits, 1u) <= 0) {  // no idle helper here: keep the item
+    atomicAdd(box + kMigCredits, 1u);
+    return false;
+  }
+  const uint32_t cap = V.mig_cap / kMigBoxes;
+  const uint32_t idx = atomicAdd(box + kMigPush, 1u);
+  if (idx >= cap) {  // this mailbox's queue is full (its helpers never look past cap)
+    atomicAdd(box + kMigCredits, 1u);
+    return false;
+  }
+  MigRec &r = V.mig_q[m * cap + idx];
+  r.state = g.state;
+  r.n = g.n;
+  r.pix = (uint32_t)pix, r.seg = seg, r.s = s, r.tc = tc, r.st = st;
+  r.acc[0] = acc.x, r.acc[1] = acc.y, r.acc[2] = acc.z;
+  __hip_atomic_store(&r.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// A wave whose lanes have all finished: run the migrated items of its mailbox until every item of
+// the launch is done.
+template <int kMode>
+__device__ __attribute__((noinline)) void mig_help(const Book1View &V, const float4 *items9, uint8_t *__restrict__ out,
+                                                 int64_t total_own) {
+  const bool l0 = __lane_id() == 0;
+  const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) / 64;
+  const uint32_t m = wave % kMigBoxes;
+  uint32_t *box = mig_box(V, m);
+  const uint32_t cap = V.mig_cap / kMigBoxes;
+  int rank = 0;
+  if (l0) rank = (int)atomicAdd(&V.mig[kMigHelpers], 1u);  // waves finished before this one
+  rank = __builtin_amdgcn_readfirstlane(rank);
+  if (rank >= V.mig_max_help) return;  // enough helpers: this wave leaves (its CU may idle)
+  if (l0) atomicAdd(box + kMigCredits, 1u);
+  uint64_t idle_since = wall_clock64();
+  for (;;) {
+    int got = -1, fin = 0;
+    if (l0) {
+      const uint32_t p = ld_rel(box + kMigPop);
+      uint32_t q = ld_rel(box + kMigPush);
+      fin = (int)ld_rel(box + kMigFinished);
+      q = q < cap ? q : cap;
+      if (p < q && atomicCAS(box + kMigPop, p, p + 1u) == p) got = (int)p;
+    }
+    got = __builtin_amdgcn_readfirstlane(got);
+    if (got >= 0) {
+      const MigRec *q = &V.mig_q[m * cap + (uint32_t)got];
+      while (__hip_atomic_load(&q->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != V.mig_epoch)
+        __builtin_amdgcn_s_sleep(1);
+      MigRec r = *q;
+      r.pix = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.pix);
+      r.seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.seg);
+      __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
+      render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
+      __builtin_amdgcn_s_setprio(0);
+      if (l0) {
+        mig_item_done(V, total_own);
+        atomicAdd(box + kMigCredits, 1u);
+      }
+      idle_since = wall_clock64();
+      continue;
+    }
+    if (__builtin_amdgcn_readfirstlane(fin)) break;
+    // (a bound on the wait, so that a protocol bug cannot hang the GPU: no launch idles a helper for
+    // seconds; the image would then be wrong, which the parity tests report)
+    if (wall_clock64() - idle_since > 400000000ull) break;  // 4 s at 100 MHz
+    for (int k = 0; k < V.mig_sleep; k++) __builtin_amdgcn_s_sleep(127);  // ~3.4 us each
+  }
 }
 
 // The whole-wave kernel (rt_book1_wave_kernel), launched on a second stream next to the lane kernel:
@@ -820,6 +945,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const float tmin = 1e-3f;
 
   int mode = kWait;
+  bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
+  uint64_t mig_next = 0;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
   int32_t pix = 0;  // (< 2^31: host-checked)
@@ -869,6 +996,22 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       continue;
     }
     if (mode != kWait) continue;
+    // migration: the work items are gone (a lane of this wave found none) and few lanes are left
+    // and enough of the GPU idles (more than mig_idle waves have become helpers): before that,
+    // whole-wave traces would take issue slots from lanes that still make full use of them.  The
+    // helper count is read at most every ~20 us per wave (a device-scope load per shading pass from
+    // every sparse wave measured 25 % slower lanes: one hot line).
+    bool mig_try = false;
+    if (kMode == kMigMode && V.mig_live > 0 && live < 64 && live <= V.mig_live) {
+      if (!mig_ok) {
+        const uint64_t now = wall_clock64();
+        if (now >= mig_next) {
+          mig_ok = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.mig_idle;  // (the count only grows)
+          mig_next = now + 2000u;
+        }
+      }
+      mig_try = mig_ok;
+    }
     // ---------------- shading pass (Camera_ray_color body after hit(), src/raytracing.c:44-75)
     bool need_pixel = !have_result, need_sample = false;
     if (have_result) {
@@ -904,6 +1047,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           if (kMode == 1) V.cost_out[pix] = px_steps;
           if (kMode == 1) V.draw_out[pix] = g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+          if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;
         } else {
           need_sample = true;
@@ -956,8 +1100,14 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }
       if (kMode == 2 && chain_boundary(V, pix, seg, g.n, (uint32_t)s, acc, tc, st, out, true)) {
+        if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
         need_pixel = true;  // this item is finished
         continue;
+      }
+      if (mig_try && !need_pixel && mig_push(V, (uint32_t)glane % kMigBoxes, pix, seg, (uint32_t)s, acc, g, tc, st)) {
+        mode = kExit;  // handed over at this sample boundary
+        need_sample = false;
+        break;
       }
       // camera ray (src/raytracing.c:96-122)
       const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
@@ -985,6 +1135,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         s++;
         if (kMode != 2 && s == spp) {
           write_pixel(out + pix * 3, acc, spp);
+          if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;
         } else {
           need_sample = true;
@@ -1002,6 +1153,17 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     L.cur = 0u;
     have_result = true;
     mode = V.n_items9 > 0 ? kTrav : kWait;
+  }
+  if (kMode == kMigMode && V.mig_live > 0) {
+    // (not inlined, so that the whole-wave code does not enlarge the lane loop's register budget;
+    // the view is passed as its kernel argument's address -- V is the kernels' first argument --
+    // because taking V's address would copy it to scratch for the whole kernel)
+#if defined(__HIP_DEVICE_COMPILE__)
+    const Book1View *Vk = (const Book1View *)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const Book1View *Vk = &V;
+#endif
+    mig_help<kMode>(*Vk, items9, out, total_own);
   }
 }
 

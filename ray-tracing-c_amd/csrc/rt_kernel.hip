@@ -529,6 +529,9 @@ __global__ void chain_fill_kernel(const uint32_t *cnt, uint32_t *ch_end, uint32_
     ch_end[i] = b1::kRecFill;
 }
 
+constexpr size_t kCounterBytes = 128 + b1::kMigWords * sizeof(uint32_t);  // work counter line + migration words
+constexpr size_t kCounterSlot = (kCounterBytes + 255) / 256 * 256;
+
 // ------------------------------------------------------------------------------ configuration
 static bool env_flag(const char *name, bool dflt) {
   const char *e = getenv(name);
@@ -559,8 +562,18 @@ struct Config {
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
   int gen_batch = 56, gen_steps = 8, gen_lds = 1024;
+  int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
+  int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
+  int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
+  int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   static Config from_env() {
     Config c;
+    c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
+    c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
+    c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
+    if (c.mig_sleep < 1) c.mig_sleep = 1;
+    c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
+    c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
     c.general = env_flag("RT_GENERAL", true);
@@ -630,6 +643,8 @@ struct rt_device_scene {
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
   uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
+  b1::MigRec *mig_q = nullptr;   // tail migration queue (rt_book1.h: MigRec)
+  uint32_t mig_epoch = 0;        //   its entries are tagged with a per-launch epoch
   uint32_t *px_time = nullptr;   // RT_PX_TIME diagnostic: {start, end} per work item
   uint32_t *seg_time = nullptr;  //   and per chain segment
   int g_grid = 0;                // group kernel: resident workgroups, LDS bytes per workgroup
@@ -980,7 +995,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   const int chunks = (s->camera.max_depth + 3) / 4 - 2;
   const size_t spill_bytes = (size_t)(chunks > 0 ? chunks : 0) * spill_lanes * sizeof(uint64_t);
   const size_t npix = (size_t)s->camera.width * s->camera.height;
-  const size_t sizes[10] = {items_bytes, H.mats.size() * sizeof(b1::FastMat), 256, spill_bytes,
+  const size_t sizes[10] = {items_bytes, H.mats.size() * sizeof(b1::FastMat), kCounterSlot, spill_bytes,
                             npix * sizeof(uint32_t),   // [4] pre-pass cost
                             npix * sizeof(int32_t),    // [5] LPT order
                             kLptHistBytes,             // [6] LPT buckets
@@ -1006,7 +1021,15 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.n_items9 = (int32_t)(H.items9.size() / 2) - 1;  // without the trailing pad item
   V.n_items9_alloc = (int32_t)(H.items9.size() / 2);
   V.mats = (const b1::FastMat *)(b + off[1]);
-  V.work_counter = (int32_t *)(b + off[2]);
+  V.work_counter = (int32_t *)(b + off[2]);  // (the counter; the migration words from the next line on)
+  V.mig = (uint32_t *)(b + off[2] + 128);
+  V.mig_live = cfg.mig_live;
+  if (cfg.mig_live > 0) {  // one queue entry per lane of the grid: an item migrates at most once per launch...
+    V.mig_cap = (uint32_t)spill_lanes;  // ...and only against an idle helper wave (push beyond: the lane keeps it)
+    HIP_OK(hipMalloc(&d->mig_q, (size_t)V.mig_cap * sizeof(b1::MigRec)));
+    HIP_OK(hipMemset(d->mig_q, 0, (size_t)V.mig_cap * sizeof(b1::MigRec)));  // epoch 0: no entry
+    V.mig_q = d->mig_q;
+  }
   V.spill = (uint64_t *)(b + off[3]);
   V.spill_lanes = spill_lanes;
   V.shade_batch = cfg.shade_batch;
@@ -1198,6 +1221,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->px_time) (void)hipFree(d->px_time);
   if (d->seg_time) (void)hipFree(d->seg_time);
+  if (d->mig_q) (void)hipFree(d->mig_q);
   if (d->pre_arena) (void)hipFree(d->pre_arena);
   if (d->ch_arena) (void)hipFree(d->ch_arena);
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
@@ -1212,6 +1236,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
 
 // ------------------------------------------------------------------------------ launches
 static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st) {
+  (void)hipMemsetAsync(P.work_counter, 0, kCounterBytes, st);  // (the previous launch left it past its items)
   P.S.cam.spp = d->cfg.lpt_spp;
   P.cost_out = d->lpt_cost;
   P.draw_out = d->draw_out;
@@ -1323,11 +1348,15 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.n_coop = d->ch_cnt + kCnNCoop;
   V.coop_counter = (int32_t *)(d->ch_cnt + kCnCoopCounter);
   V.coop_waves_dev = d->ch_cnt + kCnCoopWaves;
+  V.mig_epoch = ++d->mig_epoch;
+  V.mig_idle = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_idle / 100);
+  V.mig_sleep = cfg.mig_sleep;
+  V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
   const bool lds = d->b1_lds_bytes != 0;
   if (lds) launch_wave_kernel(d, V, d_out, st, 2, d->chain_grid);
-  HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+  HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, d->b1_lds_bytes, st, V, d_out);
   else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, V, d_out);
   HIP_OK(hipGetLastError());
@@ -1339,6 +1368,19 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   if (cfg.debug) {
     for (auto &e : dbg_ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventRecord(dbg_ev[0], st));
+    if (V.mig) {
+      std::vector<uint32_t> mw(b1::kMigWords);
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(mw.data(), V.mig, mw.size() * 4, hipMemcpyDeviceToHost));
+      uint64_t pushed = 0, popped = 0;
+      for (int m = 0; m < b1::kMigBoxes; m++) {
+        const uint32_t *bx = &mw[b1::kMigBox0 + m * b1::kMigBoxWords];
+        pushed += bx[b1::kMigPush] < V.mig_cap / b1::kMigBoxes ? bx[b1::kMigPush] : V.mig_cap / b1::kMigBoxes;
+        popped += bx[b1::kMigPop];
+      }
+      fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u\n", mw[b1::kMigHelpers],
+              (unsigned long long)pushed, (unsigned long long)popped, mw[b1::kMigDone]);
+    }
   }
   hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 4 + 1 < 2048 ? npix / 4 + 1 : 2048)), dim3(256), 0, st,
                      V, d_out, (const uint32_t *)d->ch_split, (const uint32_t *)d->ch_cnt, d->ch_cont,
@@ -1349,7 +1391,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   C.n_coop = nullptr;
   C.ch_cont = d->ch_cont;
   C.ch_n_cont = d->ch_cnt + kCnCont;
-  HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+  C.mig_epoch = ++d->mig_epoch;
+  HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, d->b1_lds_bytes, st, C, d_out);
   else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, C, d_out);
   HIP_OK(hipGetLastError());
@@ -1363,6 +1406,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
     HIP_OK(hipEventElapsedTime(&t_cont, dbg_ev[1], dbg_ev[2]));
     for (auto &e : dbg_ev) HIP_OK(hipEventDestroy(e));
     fprintf(stderr, "[rtc] chain launch ms: chains %.2f fold %.2f continuations %.2f\n", t_chains, t_fold, t_cont);
+
     uint32_t c[16];
     HIP_OK(hipStreamSynchronize(st));
     HIP_OK(hipMemcpy(c, d->ch_cnt, sizeof c, hipMemcpyDeviceToHost));
@@ -1432,7 +1476,7 @@ static int launch_lane(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipS
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool waves = V.n_coop != nullptr;
   if (waves) launch_wave_kernel(d, V, d_out, st, 0, use_group ? d->g_grid : d->b1_grid);
-  HIP_OK(hipMemsetAsync(V.work_counter, 0, sizeof(int32_t), st));
+  HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   if (use_group) {  // eight lanes per pixel (rt_group.h)
     const dim3 gg((unsigned)d->g_grid), gb(grp::kBlock);
     if (lds) hipLaunchKernelGGL((rt_book1_group_kernel<true>), gg, gb, d->g_lds_bytes, st, V, d_out);
