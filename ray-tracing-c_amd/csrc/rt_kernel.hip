@@ -72,13 +72,13 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
 }
 
 // Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.
-template <bool kLds>
-__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
-template <bool kLds>
-__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 2>(V, out, lds);
 }
@@ -566,9 +566,13 @@ struct Config {
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
+  int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
+  int lane_occ = 5;   // lane kernel occupancy target
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
+    c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ) == 5 ? 5 : 4;
+    c.lane_occ = env_int("RT_LANE_OCC", c.lane_occ) == 4 ? 4 : 5;
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -974,6 +978,8 @@ extern "C" int rt_device_count(void) {
 extern "C" void rt_scene_release(rt_device_scene *d);
 
 // Book-1 device state: the pack's arrays, the persistent grids, the LPT and chain scratch.
+static const void *chain_kernel_fn(bool lds, int occ);
+
 static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPack &H) {
   const Config &cfg = d->cfg;
   const size_t items_bytes = H.items9.size() * sizeof(float4);
@@ -983,10 +989,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0, per_cu_chain = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock, d->b1_lds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
+      &per_cu,
+      cfg.lane_occ == 4 ? (lds ? (const void *)rt_book1_kernel<true, 4> : (const void *)rt_book1_kernel<false, 4>)
+                        : (lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>),
       b1::kBlock, d->b1_lds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_chain, chain_kernel_fn(lds, cfg.chain_occ), b1::kBlock,
+                                                     d->b1_lds_bytes));
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   const int spill_grid = d->b1_grid > d->chain_grid ? d->b1_grid : d->chain_grid;
@@ -1265,6 +1273,23 @@ static void launch_wave_kernel(rt_device_scene *d, const b1::Book1View &V, uint8
   }
 }
 
+// The chain kernel's variants: LDS / global scene, and its occupancy target (launch bounds)
+static const void *chain_kernel_fn(bool lds, int occ) {
+  if (occ == 4) return lds ? (const void *)rt_book1_chain_kernel<true, 4> : (const void *)rt_book1_chain_kernel<false, 4>;
+  return lds ? (const void *)rt_book1_chain_kernel<true, 5> : (const void *)rt_book1_chain_kernel<false, 5>;
+}
+static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
+  const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
+  const size_t lds = d->b1_lds_bytes;
+  if (d->cfg.chain_occ == 4) {
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 4>), gc, blk, lds, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 4>), gc, blk, 0, st, V, d_out);
+  } else {
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 5>), gc, blk, lds, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 5>), gc, blk, 0, st, V, d_out);
+  }
+}
+
 // Records of a chain launch: grown on demand, up to the RT_CHAIN_MB budget (the planner keeps
 // pixels whole when they run out).
 static int chain_records(rt_device_scene *d, size_t npix, int spp) {
@@ -1353,12 +1378,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_sleep = cfg.mig_sleep;
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
-  const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
   const bool lds = d->b1_lds_bytes != 0;
   if (lds) launch_wave_kernel(d, V, d_out, st, 2, d->chain_grid);
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
-  if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, d->b1_lds_bytes, st, V, d_out);
-  else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, V, d_out);
+  launch_chain_kernel(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   if (lds) {
     HIP_OK(hipEventRecord(d->ev_join, d->wave_stream));
@@ -1393,8 +1416,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   C.ch_n_cont = d->ch_cnt + kCnCont;
   C.mig_epoch = ++d->mig_epoch;
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
-  if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, d->b1_lds_bytes, st, C, d_out);
-  else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, C, d_out);
+  launch_chain_kernel(d, C, d_out, st);
   HIP_OK(hipGetLastError());
   if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
   if (cfg.debug) {
@@ -1483,8 +1505,13 @@ static int launch_lane(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipS
     else hipLaunchKernelGGL((rt_book1_group_kernel<false>), gg, gb, d->g_lds_bytes, st, V, d_out);
   } else {
     const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-    if (lds) hipLaunchKernelGGL((rt_book1_kernel<true>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_kernel<false>), g1, blk, 0, st, V, d_out);
+    if (cfg.lane_occ == 4) {
+      if (lds) hipLaunchKernelGGL((rt_book1_kernel<true, 4>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+      else hipLaunchKernelGGL((rt_book1_kernel<false, 4>), g1, blk, 0, st, V, d_out);
+    } else {
+      if (lds) hipLaunchKernelGGL((rt_book1_kernel<true, 5>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+      else hipLaunchKernelGGL((rt_book1_kernel<false, 5>), g1, blk, 0, st, V, d_out);
+    }
   }
   HIP_OK(hipGetLastError());
   if (waves) {
@@ -1520,9 +1547,9 @@ static int pick_mode(const rt_device_scene *d, int64_t npix) {
   if (cfg.mode == kModeChain) return chain_ok ? kModeChain : kModeLane;
   if (cfg.mode == kModeGroup) return d->g_grid > 0 ? kModeGroup : kModeLane;
   if (cfg.mode == kModeLane) return kModeLane;
-  // auto: the chain render when the launch has fewer than two pixels per lane (a frame split over
-  // GPUs); with more, the lane kernel's longest-first order already keeps the lanes busy
-  return chain_ok && npix < 2 * (int64_t)d->chain_grid * b1::kBlock ? kModeChain : kModeLane;
+  // auto: the chain render whenever it applies (measured ahead of the lane kernel at every N, from
+  // 1.16x at N = 1 to 2.2x at N = 8: DESIGN.md §5); the lane kernel for low spp / small launches
+  return chain_ok ? kModeChain : kModeLane;
 }
 
 static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows, uint8_t *d_out, hipStream_t st) {
