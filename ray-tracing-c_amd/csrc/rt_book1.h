@@ -880,6 +880,23 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
   }
 }
 
+// A chain launch's whole-wave items (the first *n_coop of ch_items), claimed one per wave through
+// coop_counter by the chain kernel's first *coop_waves_dev waves.  Not inlined (see mig_help).
+__device__ __attribute__((noinline)) void coop_items(const Book1View &V, const float4 *items9,
+                                                   uint8_t *__restrict__ out) {
+  const int64_t n_coop = (int64_t)*V.n_coop;
+  for (;;) {
+    int k = 0;
+    if (__lane_id() == 0) k = atomicAdd(V.coop_counter, 1);
+    k = __shfl(k, 0);
+    if (k >= n_coop) break;
+    __builtin_amdgcn_s_setprio(3);  // these chains set the frame time: issue before the lane-parallel waves
+    const uint2 it = V.ch_items[k];
+    render_item_coop<2>(V, items9, (int64_t)it.x, it.y, out);
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 // The whole-wave kernel (rt_book1_wave_kernel), launched on a second stream next to the lane kernel:
 // its first *coop_waves_dev waves claim the first *n_coop items, one item per wave, heaviest first.
 // A kernel of its own, so that the whole-wave code's registers do not count against the lane
@@ -922,8 +939,10 @@ constexpr int kSteps = 4;
 template <bool kLds, int kMode = 0>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
-  // the last workgroups of the grid leave their CU slots to the whole-wave kernel (render_wave_items)
-  if (V.n_coop != nullptr && (int)blockIdx.x >= (int)gridDim.x - (int)((*V.coop_waves_dev + kWaves - 1) / kWaves))
+  // lane launches: the last workgroups of the grid leave their CU slots to the whole-wave kernel
+  // (render_wave_items); chain launches run their whole-wave items in the grid's first waves (below)
+  if (kMode != 2 && V.n_coop != nullptr &&
+      (int)blockIdx.x >= (int)gridDim.x - (int)((*V.coop_waves_dev + kWaves - 1) / kWaves))
     return;
   const bool cont = kMode == 2 && V.ch_cont != nullptr;
   if (cont && *V.ch_n_cont == 0u) return;  // (before staging the scene: the usual continuation launch is empty)
@@ -938,6 +957,17 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   }
   const int glane = blockIdx.x * kBlock + tid;
   const int lane = __lane_id();
+  if (kMode == 2 && V.n_coop != nullptr && glane / 64 < (int)*V.coop_waves_dev) {
+    // the chain launch's whole-wave items (heaviest first), in this kernel's first waves: a second
+    // kernel next to this one got its CU slots only once workgroups of this one had finished
+    // (measured: whole-wave items starting at 64 ms of a 106-ms launch); then on to lane items
+#if defined(__HIP_DEVICE_COMPILE__)
+    const Book1View *Vk = (const Book1View *)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const Book1View *Vk = &V;
+#endif
+    coop_items(*Vk, items9, out);
+  }
   const rt_camera &cam = V.S.cam;
   const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
   const bool dof = cam.dof_angle > 0.0f;

@@ -472,19 +472,10 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
   cnt[kCnNCoop] = n_wave;
   cnt[kCnWaveNext] = 0;
   cnt[kCnCoopCounter] = 0;
-  uint32_t W = 0;
-  if (n_wave > 0) {  // balance the whole-wave queue against the lanes (throughput), in wave counts
-    double total = 0.0;
-    for (int k = 0; k < 256; k++) total += (double)sums[k];
-    const double V = (double)*(const unsigned long long *)&cnt[kCnWaveWork], L = fmax(0.0, total - V);
-    const double G = (double)m.grid_waves;
-    double w = 64.0 * V * m.coop * G / (L * m.thr + 64.0 * V * m.coop);
-    w = fmin(fmax(w, 4.0), G / 2.0);
-    W = ((uint32_t)ceil(w) + 3u) & ~3u;
-    const uint32_t n4 = (n_wave + 3u) & ~3u;
-    if (W > n4) W = n4;
-  }
-  cnt[kCnCoopWaves] = W;
+  // every whole-wave item gets a wave of the chain kernel from the start (up to half the grid): they
+  // are the launch's longest chains, and a wave that runs out of them goes on to lane items
+  const uint32_t half = (uint32_t)m.grid_waves / 2u;
+  cnt[kCnCoopWaves] = n_wave < half ? n_wave : half;
 }
 
 __global__ void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk, uint2 *items,
@@ -1379,14 +1370,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
-  if (lds) launch_wave_kernel(d, V, d_out, st, 2, d->chain_grid);
+  if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
-  launch_chain_kernel(d, V, d_out, st);
+  launch_chain_kernel(d, V, d_out, st);  // (whole-wave items in its first waves: rt_book1.h coop_items)
   HIP_OK(hipGetLastError());
-  if (lds) {
-    HIP_OK(hipEventRecord(d->ev_join, d->wave_stream));
-    HIP_OK(hipStreamWaitEvent(st, d->ev_join, 0));
-  }
   hipEvent_t dbg_ev[3] = {nullptr, nullptr, nullptr};  // (RT_DEBUG: chains / fold / continuations)
   if (cfg.debug) {
     for (auto &e : dbg_ev) HIP_OK(hipEventCreate(&e));
