@@ -125,6 +125,7 @@ struct Book1View {
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
   const int32_t *order;      // work item order (longest-first from the cost pre-pass), or null
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
+  uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // the first *n_coop items (of `order` / ch_items) go to whole waves
   int32_t *coop_counter;     //   (render_pixel_coop), claimed through this counter
@@ -1072,10 +1073,13 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         else
           acc = add(acc, col);
         s++;
-        if (kMode != 2 && s == spp) {  // quantize (src/raytracing.c:127-131)
-          write_pixel(out + pix * 3, acc, spp);
-          if (kMode == 1) V.cost_out[pix] = px_steps;
-          if (kMode == 1) V.draw_out[pix] = g.n;
+        // (the cost pre-pass stops a pixel early once it has spent cost_budget steps: its cost and
+        // draws are extrapolated from the samples done, and the pre-pass's latency stays bounded)
+        const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
+        if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
+          if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
+          if (kMode == 1) V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
+          if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;

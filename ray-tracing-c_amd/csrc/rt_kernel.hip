@@ -478,17 +478,37 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
   cnt[kCnCoopWaves] = n_wave < half ? n_wave : half;
 }
 
-__global__ void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk, uint2 *items,
-                                     uint64_t *wave_key) {
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-    const uint32_t K = kk[p] & 0xffffu;
-    const bool wave = (kk[p] >> 31) != 0u;
-    const uint32_t cc = cost[p] / K;
-    const uint32_t at = wave ? atomicAdd(&cnt[kCnWaveNext], K) : atomicAdd(&cnt[kCnOff + lpt_bucket(cc)], K);
-    for (uint32_t k = 0; k < K; k++) {
-      items[at + k] = make_uint2((uint32_t)p, K == 1u ? b1::kItemUnsplit : k);
-      if (wave) wave_key[at + k] = ((uint64_t)cc << 32) | (uint32_t)(0xffffffffu - (at + k));
+__global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk,
+                                                            uint2 *items, uint64_t *wave_key) {
+  // two-level: the block's items per bucket are counted in LDS, one global atomic per bucket and
+  // block reserves their range (one global atomic per pixel on 256 bucket words serialised: 3 ms
+  // for a full frame)
+  __shared__ uint32_t cnt_l[257], base_l[257];
+  const int stride = gridDim.x * blockDim.x;
+  for (int p0 = blockIdx.x * blockDim.x; p0 < n; p0 += stride) {
+    for (int k = threadIdx.x; k < 257; k += blockDim.x) cnt_l[k] = 0u;
+    __syncthreads();
+    const int p = p0 + (int)threadIdx.x;
+    uint32_t K = 0u, b = 256u, loc = 0u, cc = 0u;
+    if (p < n) {
+      K = kk[p] & 0xffffu;
+      const bool wave = (kk[p] >> 31) != 0u;
+      cc = cost[p] / K;
+      b = wave ? 256u : lpt_bucket(cc);  // 256: the whole-wave list
+      loc = atomicAdd(&cnt_l[b], K);
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 257; k += blockDim.x)
+      if (cnt_l[k]) base_l[k] = atomicAdd(k == 256 ? &cnt[kCnWaveNext] : &cnt[kCnOff + k], cnt_l[k]);
+    __syncthreads();
+    if (p < n) {
+      const uint32_t at = base_l[b] + loc;
+      for (uint32_t k = 0; k < K; k++) {
+        items[at + k] = make_uint2((uint32_t)p, K == 1u ? b1::kItemUnsplit : k);
+        if (b == 256u) wave_key[at + k] = ((uint64_t)cc << 32) | (uint32_t)(0xffffffffu - (at + k));
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -559,11 +579,13 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
   int lane_occ = 5;   // lane kernel occupancy target
+  int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
     c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ) == 5 ? 5 : 4;
     c.lane_occ = env_int("RT_LANE_OCC", c.lane_occ) == 4 ? 4 : 5;
+    c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -1239,6 +1261,7 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.S.cam.spp = d->cfg.lpt_spp;
   P.cost_out = d->lpt_cost;
   P.draw_out = d->draw_out;
+  P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.order = nullptr;
   P.n_coop = nullptr;
   const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
