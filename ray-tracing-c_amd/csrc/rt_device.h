@@ -37,6 +37,7 @@ constexpr float kPi = 3.14159265358979323846f;      // (float)M_PI
 constexpr float kInvPi = 0.318309886183790671538f;  // (float)M_1_PI
 constexpr int kStackMax = 48;                       // DFS stack slots (flattener checks need <= this)
 constexpr int kMaxDepth = 64;                       // path record slots (host checks max_depth)
+constexpr int kMaxDepthDeep = 1 << 16;              // beyond kMaxDepth: rt_render_deep_kernel
 
 // ------------------------------------------------------------------------------ vectors
 struct f3 {
@@ -815,12 +816,20 @@ RT_D float lights_pdf(const DScene &S, f3 o, f3 d) {
 // Camera_ray_color (src/raytracing.c:39-84) unrolled into a loop.  Each scattering bounce k
 // records (e_k, a_k, w_k); when the path ends with tail value c, the colour is folded
 // innermost-first: c = e_k + (a_k * c) [* w_k], which is the recursion's evaluation order.
-template <int F>
-RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
+// Paths longer than kMaxDepth (kDeep): the record lives in a caller-provided global-memory slot of
+// max_depth entries instead of registers / scratch (rt_render_deep_kernel).
+struct DeepRec {
+  f3 a, e;
+  float w;
+  uint32_t weighted;
+};
+
+template <int F, bool kDeep = false>
+RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g, DeepRec *deep = nullptr) {
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
-  f3 rec_a[kMaxDepth];
-  f3 rec_e[kFull ? kMaxDepth : 1];
-  float rec_w[kFull ? kMaxDepth : 1];
+  f3 rec_a[kDeep ? 1 : kMaxDepth];
+  f3 rec_e[kFull && !kDeep ? kMaxDepth : 1];
+  float rec_w[kFull && !kDeep ? kMaxDepth : 1];
   uint64_t weighted = 0;
   int n = 0;
   f3 tail;
@@ -844,17 +853,24 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
       tail = e;
       break;
     }
-    rec_a[n] = albedo;
+    if (kDeep) deep[n].a = albedo, deep[n].weighted = 0u;
+    else rec_a[n] = albedo;
     if (kFull) {
-      rec_e[n] = e;
+      if (kDeep) deep[n].e = e;
+      else rec_e[n] = e;
       // mixture pdf (src/raytracing.c:56-71): only when the scene has lights and p != 0 (runtime bit:
       // a kernel variant compiled with the LIGHTS path may run a scene without lights)
       if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
         if (g.f32() < prob) out = lights_rand(S, r.p, g);
         const float sp = scatter_pdf(S, r.material, r.normal, out);
         const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, out);
-        rec_w[n] = sp / spdf;
-        weighted |= 1ull << n;
+        if (kDeep) {
+          deep[n].w = sp / spdf;
+          deep[n].weighted = 1u;
+        } else {
+          rec_w[n] = sp / spdf;
+          weighted |= 1ull << n;
+        }
       }
     }
     n++;
@@ -863,10 +879,10 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
   }
   f3 c = tail;
   for (int k = n - 1; k >= 0; k--) {
-    f3 x = mul(rec_a[k], c);
+    f3 x = mul(kDeep ? deep[k].a : rec_a[k], c);
     if (kFull) {
-      if ((weighted >> k) & 1) x = scale(x, rec_w[k]);
-      c = add(rec_e[k], x);
+      if (kDeep ? deep[k].weighted != 0u : ((weighted >> k) & 1) != 0) x = scale(x, kDeep ? deep[k].w : rec_w[k]);
+      c = add(kDeep ? deep[k].e : rec_e[k], x);
     } else {
       c = add(mk(0.0f, 0.0f, 0.0f), x);
     }
@@ -877,8 +893,8 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g) {
 // ------------------------------------------------------------------------------ one pixel
 // Camera_render's per-pixel body (src/raytracing.c:93-131): seed, spp samples (jitter, thin-lens
 // disc, primary ray, path colour), mean, gamma 2, clamp-macro semantics (NaN -> 0), truncation.
-template <int F>
-RT_D void render_pixel(const DScene &S, int i, int j, uint8_t *dst) {
+template <int F, bool kDeep = false>
+RT_D void render_pixel(const DScene &S, int i, int j, uint8_t *dst, DeepRec *deep = nullptr) {
   Pcg32 g;
   g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));
   const f3 du = ld3(S.cam.delta_u), dv = ld3(S.cam.delta_v), lf = ld3(S.cam.origin);
@@ -899,7 +915,7 @@ RT_D void render_pixel(const DScene &S, int i, int j, uint8_t *dst) {
       o = add(add(lf, scale(ld3(S.cam.disc_u), a)), scale(ld3(S.cam.disc_v), b));
     }
     const f3 d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
-    acc = add(acc, path_color<F>(S, o, d, g));
+    acc = add(acc, path_color<F, kDeep>(S, o, d, g, deep));
   }
   const float spp_f = (float)S.cam.spp;
   const float ch[3] = {acc.x, acc.y, acc.z};

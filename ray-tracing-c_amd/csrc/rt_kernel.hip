@@ -71,6 +71,21 @@ __global__ __launch_bounds__(kBlock) void rt_render_rows_kernel(DScene S, int ro
   render_pixel<F>(S, i, row0 + jj * row_stride, out + pix * 3);
 }
 
+// max_depth > kMaxDepth: one pixel per thread, grid-stride over the launch, the path record in a
+// global-memory slot of max_depth entries per thread (rt_device.h: DeepRec).
+template <int F>
+__global__ __launch_bounds__(kBlock) void rt_render_deep_kernel(DScene S, int row0, int row_stride, int n_rows,
+                                                                uint8_t *__restrict__ out, DeepRec *rec) {
+  const int W = S.cam.width;
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x, nthreads = (int64_t)gridDim.x * kBlock;
+  DeepRec *mine = rec + tid * S.cam.max_depth;
+  for (int64_t pix = tid; pix < (int64_t)n_rows * W; pix += nthreads) {
+    const int jj = (int)(pix / W);
+    const int i = (int)(pix - (int64_t)jj * W);
+    render_pixel<F, true>(S, i, row0 + jj * row_stride, out + pix * 3, mine);
+  }
+}
+
 // Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.
 template <bool kLds, int kOcc = 5>
 __global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
@@ -660,6 +675,8 @@ struct rt_device_scene {
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
   uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
+  DeepRec *deep_rec = nullptr;   // max_depth > kMaxDepth: path records (rt_render_deep_kernel)
+  int64_t deep_threads = 0;
   b1::MigRec *mig_q = nullptr;   // tail migration queue (rt_book1.h: MigRec)
   uint32_t mig_epoch = 0;        //   its entries are tagged with a per-launch epoch
   uint32_t *px_time = nullptr;   // RT_PX_TIME diagnostic: {start, end} per work item
@@ -710,8 +727,8 @@ static bool ref_ok(const rt_flat_scene *s, int32_t ref, bool allow_none) {
 static int validate(const rt_flat_scene *s) {
   const rt_camera &c = s->camera;
   if (c.width <= 0 || c.height <= 0 || c.spp <= 0) return rt_set_error("bad image size / spp"), -1;
-  if (c.max_depth > kMaxDepth)
-    return rt_set_error("max_depth %d exceeds the kernel's path record (%d)", c.max_depth, kMaxDepth), -1;
+  if (c.max_depth > kMaxDepthDeep)
+    return rt_set_error("max_depth %d exceeds the deep kernel's path record (%d)", c.max_depth, kMaxDepthDeep), -1;
   if (s->stack_needed > kStackMax)
     return rt_set_error("scene needs %d traversal stack slots, kernel has %d", s->stack_needed, kStackMax), -1;
   if (!ref_ok(s, s->root, false) || rt_ref_kind(s->root) != RT_KIND_LIST) return rt_set_error("bad root"), -1;
@@ -1220,6 +1237,20 @@ static rt_device_scene *upload_packed(const rt_flat_scene *s, const HostPack &H,
     rt_scene_release(d);
     return NULL;
   }
+  if (s->camera.max_depth > kMaxDepth) {  // deep paths: rt_render_deep_kernel and its record slots
+    const size_t per = (size_t)s->camera.max_depth * sizeof(DeepRec);
+    const size_t npix = (size_t)s->camera.width * s->camera.height;
+    size_t threads = ((size_t)1 << 30) / per;  // 1 GiB of records
+    threads = threads < npix ? threads : npix;
+    threads = (threads + kBlock - 1) / kBlock * kBlock;
+    if (hipMalloc(&d->deep_rec, threads * per) != hipSuccess) {
+      rt_set_error("hipMalloc of the deep path records failed on device %d", device);
+      rt_scene_release(d);
+      return NULL;
+    }
+    d->deep_threads = (int64_t)threads;
+    return d;
+  }
   if (!d->book1 && H.cfg.general && general_upload(d, s) != 0) {
     rt_scene_release(d);
     return NULL;
@@ -1243,6 +1274,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->px_time) (void)hipFree(d->px_time);
   if (d->seg_time) (void)hipFree(d->seg_time);
   if (d->mig_q) (void)hipFree(d->mig_q);
+  if (d->deep_rec) (void)hipFree(d->deep_rec);
   if (d->pre_arena) (void)hipFree(d->pre_arena);
   if (d->ch_arena) (void)hipFree(d->ch_arena);
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
@@ -1613,6 +1645,18 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     launch_general(d, all, gg, gb, st, G, d_out);
     HIP_OK(hipGetLastError());
     if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+    return 0;
+  }
+  if (d->deep_rec) {
+    const int64_t th = d->deep_threads < npix ? (d->deep_threads + kBlock - 1) / kBlock * kBlock : npix;
+    const dim3 gd((unsigned)((th + kBlock - 1) / kBlock)), bd(kBlock);
+    if ((d->features & ~kFeatBook1) == 0)
+      hipLaunchKernelGGL(rt_render_deep_kernel<kFeatBook1>, gd, bd, 0, st, d->view, row0, row_stride, n_rows, d_out,
+                         d->deep_rec);
+    else
+      hipLaunchKernelGGL(rt_render_deep_kernel<kFeatAll>, gd, bd, 0, st, d->view, row0, row_stride, n_rows, d_out,
+                         d->deep_rec);
+    HIP_OK(hipGetLastError());
     return 0;
   }
   const dim3 grid((unsigned)((npix + kBlock - 1) / kBlock)), block(kBlock);

@@ -1,0 +1,200 @@
+/* api_worlds.c — TEST INFRASTRUCTURE.  Worlds that none of the reference driver's presets builds,
+ * made only through the reference's public C API (include/{raytracing,hittable,material,texture,
+ * vec3,pcg32}.h) and rendered with Camera_render.  The same source is linked twice:
+ *   oracle/_ref/api_worlds_ref      against the reference's own src/*.c (oracle/Makefile), run here
+ *                                   to make the fixtures tests/golden/api_*.rgb.gz;
+ *   tests/native/bin/api_worlds_gpu against librtc_amd.so (the drop-in), run by the -m gpu tests.
+ * The paths it covers (VERDICT r01 "parity on API paths outside the presets"):
+ *   0 SurfaceNormal material (src/material.c:19-20, :105, :135)
+ *   1 hollow glass: a negative-radius sphere inside a glass sphere (src/hittable.c:120-151)
+ *   2 Metal with fuzz > 1 and fuzz 0, thin-lens DOF on a sphere world (src/material.c:48-58)
+ *   3 quads, Box under RotateY + Translate, a constant medium, Checker texture, a light with
+ *     importance sampling, DOF (src/hittable.c:186-432, src/raytracing.c:56-71)
+ *   4 max_depth 100 inside a mirror sphere: most paths run to the depth limit
+ *   5 a 1-pixel-wide image (48 rows) of a BVH world
+ *   6 a flat list of 120 spheres (no BVH), Book-1 materials, 64 spp
+ *   7 max_depth 100 on a BVH world of Book-1 materials (the fast path's depth limit)
+ * usage: api_worlds <id> <out.rgb>     prints "width height" on stdout */
+#include "hittable.h"
+#include "material.h"
+#include "pcg32.h"
+#include "raytracing.h"
+#include "texture.h"
+#include "vec3.h"
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+static void camera_defaults(Camera *c, int width, float aspect, int spp, int depth) {
+  c->aspect_ratio = aspect;
+  c->img_width = width;
+  c->samples_per_pixel = spp;
+  c->max_depth = depth;
+  c->vup = vec3(0.0f, 1.0f, 0.0f);
+  c->dof_angle = 0.0f;
+  c->focal_length = 1.0f;
+  c->lights_sampling_prob = 0.5f;
+  c->background = vec3(0.70f, 0.80f, 1.00f);
+  c->vfov = 50.0f;
+  c->look_from = vec3(0.0f, 0.4f, 1.5f);
+  c->look_to = vec3(0.0f, 0.0f, -1.0f);
+}
+
+static void add(World *w, Hittable *h) { HittableList_append(&w->objects, h); }
+
+static Material *lamb(float r, float g, float b) { return Lambertian_new(Solid_new(vec3(r, g, b))); }
+
+static void ground(World *w) { add(w, Sphere_new(vec3(0.0f, -1000.5f, -1.0f), 1000.0f, lamb(0.45f, 0.5f, 0.4f))); }
+
+static void world_surface_normal(World *w, Camera *c) {
+  camera_defaults(c, 96, 16.0f / 9.0f, 40, 20);
+  ground(w);
+  add(w, Sphere_new(vec3(0.0f, 0.0f, -1.0f), 0.5f, SurfaceNormal_new()));
+  add(w, Sphere_new(vec3(-1.05f, 0.0f, -1.2f), 0.45f, lamb(0.8f, 0.3f, 0.3f)));
+  add(w, Sphere_new(vec3(1.05f, 0.0f, -1.2f), 0.45f, SurfaceNormal_new()));
+}
+
+static void world_hollow_glass(World *w, Camera *c) {
+  camera_defaults(c, 96, 16.0f / 9.0f, 64, 50);
+  ground(w);
+  add(w, Sphere_new(vec3(0.0f, 0.0f, -1.0f), 0.5f, Dielectric_new(1.5f)));
+  add(w, Sphere_new(vec3(0.0f, 0.0f, -1.0f), -0.42f, Dielectric_new(1.5f)));  // the hollow inside
+  add(w, Sphere_new(vec3(-1.0f, 0.0f, -1.4f), 0.5f, lamb(0.1f, 0.2f, 0.5f)));
+  add(w, Sphere_new(vec3(1.0f, 0.0f, -1.4f), 0.5f, Metal_new(Solid_new(vec3(0.8f, 0.6f, 0.2f)), 0.05f)));
+  add(w, Sphere_new(vec3(0.3f, -0.35f, -0.3f), 0.15f, Dielectric_new(1.0f / 1.33f)));
+}
+
+static void world_metal_fuzz(World *w, Camera *c) {
+  camera_defaults(c, 96, 16.0f / 9.0f, 48, 50);
+  c->dof_angle = 2.0f;
+  c->focal_length = 2.4f;
+  ground(w);
+  add(w, Sphere_new(vec3(-1.1f, 0.0f, -1.0f), 0.5f, Metal_new(Solid_new(vec3(0.8f, 0.8f, 0.8f)), 1.5f)));
+  add(w, Sphere_new(vec3(0.0f, 0.0f, -1.0f), 0.5f, Metal_new(Solid_new(vec3(0.7f, 0.6f, 0.5f)), 0.0f)));
+  add(w, Sphere_new(vec3(1.1f, 0.0f, -1.0f), 0.5f, Metal_new(Solid_new(vec3(0.2f, 0.5f, 0.8f)), 3.0f)));
+  add(w, Sphere_new(vec3(0.0f, -0.3f, -0.2f), 0.2f, lamb(0.9f, 0.1f, 0.1f)));
+}
+
+static void world_quads_xform(World *w, Camera *c) {
+  camera_defaults(c, 96, 1.0f, 24, 30);
+  c->background = vec3(0.02f, 0.02f, 0.03f);
+  c->dof_angle = 1.5f;
+  c->focal_length = 6.0f;
+  c->vfov = 40.0f;
+  c->look_from = vec3(2.0f, 2.5f, 6.0f);
+  c->look_to = vec3(0.0f, 0.8f, 0.0f);
+  Texture *chk = Checker_new(0.6f, Solid_new(vec3(0.2f, 0.3f, 0.1f)), Solid_new(vec3(0.9f, 0.9f, 0.9f)));
+  add(w, Quad_new(vec3(-4.0f, 0.0f, -4.0f), vec3(8.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 8.0f), Lambertian_new(chk)));
+  add(w, Quad_new(vec3(-4.0f, 0.0f, -3.0f), vec3(8.0f, 0.0f, 0.0f), vec3(0.0f, 5.0f, 0.0f), lamb(0.6f, 0.3f, 0.3f)));
+  Hittable *box = Box_new(vec3(0.0f, 0.0f, 0.0f), vec3(1.2f, 1.6f, 1.0f), lamb(0.73f, 0.73f, 0.73f));
+  box = RotateY_new(box, 25.0f);
+  box = Translate_new(box, vec3(-1.6f, 0.0f, -0.6f));
+  add(w, box);
+  Hittable *fog = Sphere_new(vec3(1.3f, 0.8f, 0.2f), 0.8f, Dielectric_new(1.5f));
+  add(w, ConstantMedium_new(fog, 0.9f, Solid_new(vec3(0.2f, 0.4f, 0.9f))));
+  add(w, Sphere_new(vec3(0.4f, 0.45f, 1.2f), 0.45f, Metal_new(Solid_new(vec3(0.9f, 0.9f, 0.9f)), 0.2f)));
+  Material *light = DiffuseLight_new(Solid_new(vec3(6.0f, 6.0f, 6.0f)));
+  Hittable *panel = Quad_new(vec3(-1.0f, 4.0f, -1.0f), vec3(2.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 2.0f), light);
+  add(w, panel);
+  HittableList_append(&w->lights, panel);
+}
+
+static void world_deep_mirror(World *w, Camera *c) {
+  camera_defaults(c, 64, 16.0f / 9.0f, 8, 100);
+  c->background = vec3(0.0f, 0.0f, 0.0f);
+  c->look_from = vec3(0.0f, 0.0f, 0.0f);
+  c->look_to = vec3(0.0f, 0.0f, -1.0f);
+  c->vfov = 80.0f;
+  // inside a near-perfect mirror: a path leaves only through the small light
+  add(w, Sphere_new(vec3(0.0f, 0.0f, 0.0f), 4.0f, Metal_new(Solid_new(vec3(0.97f, 0.96f, 0.95f)), 0.01f)));
+  add(w, Sphere_new(vec3(1.5f, 1.0f, -2.0f), 0.3f, DiffuseLight_new(Solid_new(vec3(4.0f, 3.0f, 2.0f)))));
+  add(w, Sphere_new(vec3(-1.0f, -0.8f, -2.5f), 0.6f, lamb(0.5f, 0.7f, 0.4f)));
+}
+
+static Hittable *random_bvh(int n, uint64_t seed, float spread) {
+  PCG32 rng;
+  pcg32_seed(&rng, seed, 7u);
+  Hittable *list = HittableList_new((size_t)n);
+  for (int k = 0; k < n; k++) {
+    const float x = pcg32_f32_between(&rng, -spread, spread);
+    const float z = pcg32_f32_between(&rng, -spread - 2.0f, spread - 2.0f);
+    const float r = pcg32_f32_between(&rng, 0.08f, 0.25f);
+    const float pick = pcg32_f32(&rng);
+    Material *m;
+    if (pick < 0.6f) {
+      const float g = pcg32_f32(&rng);
+      m = lamb(0.2f + 0.6f * g, 0.5f, 0.9f - 0.6f * g);
+    } else if (pick < 0.85f) {
+      m = Metal_new(Solid_new(vec3(0.8f, 0.8f, 0.7f)), pcg32_f32(&rng));
+    } else {
+      m = Dielectric_new(1.5f);
+    }
+    HittableList_append((HittableList *)list, Sphere_new(vec3(x, r - 0.5f, z), r, m));
+  }
+  return BVHNode_new((HittableList *)list, &rng);
+}
+
+static void world_one_px_wide(World *w, Camera *c) {
+  camera_defaults(c, 1, 1.0f / 48.0f, 64, 50);
+  c->vfov = 60.0f;
+  ground(w);
+  add(w, random_bvh(40, 11u, 1.5f));
+}
+
+static void world_flat_list(World *w, Camera *c) {
+  camera_defaults(c, 96, 16.0f / 9.0f, 64, 50);
+  ground(w);
+  PCG32 rng;
+  pcg32_seed(&rng, 5u, 3u);
+  for (int k = 0; k < 120; k++) {
+    const float x = pcg32_f32_between(&rng, -2.5f, 2.5f);
+    const float z = pcg32_f32_between(&rng, -4.0f, -0.5f);
+    const float r = pcg32_f32_between(&rng, 0.05f, 0.2f);
+    const float pick = pcg32_f32(&rng);
+    Material *m = pick < 0.5f ? lamb(0.3f, 0.6f, 0.3f)
+                  : pick < 0.8f ? Metal_new(Solid_new(vec3(0.9f, 0.8f, 0.8f)), 0.3f * pick)
+                                : Dielectric_new(1.5f);
+    add(w, Sphere_new(vec3(x, r - 0.5f, z), r, m));
+  }
+}
+
+static void world_bvh_depth100(World *w, Camera *c) {
+  camera_defaults(c, 96, 16.0f / 9.0f, 32, 100);
+  ground(w);
+  add(w, random_bvh(60, 23u, 2.0f));
+  add(w, Sphere_new(vec3(0.0f, 0.1f, -1.5f), 0.6f, Dielectric_new(1.5f)));
+}
+
+int main(int argc, char **argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s <world 0-7> <out.rgb>\n", argv[0]);
+    return 2;
+  }
+  World world;
+  World_init(&world, 256);
+  Camera camera;
+  switch (atoi(argv[1])) {
+    case 0: world_surface_normal(&world, &camera); break;
+    case 1: world_hollow_glass(&world, &camera); break;
+    case 2: world_metal_fuzz(&world, &camera); break;
+    case 3: world_quads_xform(&world, &camera); break;
+    case 4: world_deep_mirror(&world, &camera); break;
+    case 5: world_one_px_wide(&world, &camera); break;
+    case 6: world_flat_list(&world, &camera); break;
+    case 7: world_bvh_depth100(&world, &camera); break;
+    default: fprintf(stderr, "unknown world\n"); return 2;
+  }
+  Camera_init(&camera);
+  const size_t n = (size_t)camera.img_width * camera.img_height * 3;
+  uint8_t *img = malloc(n);
+  Camera_render(&camera, &world, img);
+  FILE *f = fopen(argv[2], "wb");
+  if (!f || fwrite(img, 1, n, f) != n) {
+    fprintf(stderr, "cannot write %s\n", argv[2]);
+    return 1;
+  }
+  fclose(f);
+  printf("%d %d\n", camera.img_width, camera.img_height);
+  return 0;
+}

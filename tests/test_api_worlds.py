@@ -1,0 +1,77 @@
+"""Parity on API paths no preset scene uses (VERDICT r01 "what's missing" 5, ADVICE r01 max_depth).
+
+tests/native/api_worlds.c builds eight worlds through the reference's public C API only
+(SurfaceNormal, a negative-radius hollow glass sphere, Metal fuzz > 1 with DOF, quads + Box under
+RotateY/Translate + a constant medium + Checker + a sampled light + DOF, max_depth 100 inside a
+mirror, a 1-pixel-wide image, a flat 120-sphere list, max_depth 100 on a BVH world) and renders them
+with Camera_render.  The fixtures in tests/golden/api/ come from the same source linked to the
+reference's own src/*.c (oracle/_ref/api_worlds_ref, tests/golden/make_api_golden.py); the GPU
+tests run the same source linked to librtc_amd.so (tests/native/bin/api_worlds_gpu) and require
+the bytes to be identical.
+"""
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "api")
+EXE = os.path.join(ROOT, "tests", "native", "bin", "api_worlds_gpu")
+MAN = json.load(open(os.path.join(GOLD, "manifest.json")))
+WORLDS = sorted(MAN["worlds"], key=int)
+# worlds the Book-1 fast path takes (spheres, Solid Lambertian / Metal / Dielectric, max_depth <= 64)
+BOOK1 = ["1", "2", "5", "6"]
+
+
+def golden(wid):
+    e = MAN["worlds"][wid]
+    data = gzip.open(os.path.join(GOLD, e["file"])).read()
+    return np.frombuffer(data, np.uint8).reshape(e["height"], e["width"], 3), e
+
+
+@pytest.mark.parametrize("wid", WORLDS)
+def test_api_golden_fixture_intact(wid):
+    img, e = golden(wid)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"]
+
+
+def test_api_worlds_binary_built():
+    assert os.access(EXE, os.X_OK), "make -C tests/native"
+
+
+def _render(wid, tmp_path, env=None):
+    out = tmp_path / f"w{wid}.rgb"
+    r = subprocess.run([EXE, wid, str(out)], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, **(env or {})})
+    assert r.returncode == 0, r.stderr[-2000:]
+    w, h = (int(x) for x in r.stdout.split())
+    return np.fromfile(out, np.uint8).reshape(h, w, 3)
+
+
+def _check(img, ref, what):
+    assert img.shape == ref.shape, what
+    bad = (img != ref).any(axis=-1)
+    if bad.any():
+        y, x = np.argwhere(bad)[0]
+        pytest.fail(f"{what}: {bad.sum()} / {bad.size} pixels differ; first at (x={x}, y={y}): "
+                    f"gpu={img[y, x].tolist()} ref={ref[y, x].tolist()}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wid", WORLDS)
+def test_gpu_api_world_matches_reference_build(wid, tmp_path):
+    ref, e = golden(wid)
+    _check(_render(wid, tmp_path), ref, f"world {wid} ({e['name']})")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"RT_MODE": "lane"}, {"RT_MODE": "group"}, {"RT_MODE": "chain", "RT_LPT_SPP": "2"},
+                                 {"RT_BOOK1": "0"}])
+@pytest.mark.parametrize("wid", BOOK1)
+def test_gpu_api_world_book1_variants(wid, env, tmp_path):
+    ref, e = golden(wid)
+    _check(_render(wid, tmp_path, env), ref, f"world {wid} ({e['name']}) {env}")

@@ -62,6 +62,45 @@ def test_gpu_north_star_frame_pixel_identical(manifest):
         pytest.fail(f"full-frame sha mismatch; crops differing: {bad}")
 
 
+@pytest.mark.parametrize("world", [8, 4, 2])
+def test_gpu_north_star_rank_shares_reassemble(manifest, world):
+    """BASELINE config 4 (the north-star frame over 8 GPUs, rows j % 8) rehearsed on one device:
+    every rank's share rendered as its own launch (the multi-GPU bench's per-rank call), then
+    reassembled: the frame's sha must equal the reference render's."""
+    import torch
+
+    e = manifest["renders"].get("s1_1200x675_1000spp_d50")
+    if e is None:
+        pytest.skip("north-star golden not generated (make_golden.py --big)")
+    sc = rtc.Scene.preset(1, 1200, 1000, 50)
+    ds = rtc.DeviceScene(sc, 0)
+    stream = torch.cuda.current_stream(0)
+    parts = []
+    for rank in range(world):
+        row0, stride, n = rtc.rows_of(sc.height, rank, world)
+        buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+        ds.render_rows_async(row0, stride, n, buf.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        parts.append(buf.cpu().numpy())
+    ds.close()
+    frame = rtc.assemble_frame(parts, sc.height, world)
+    assert hashlib.sha256(frame.tobytes()).hexdigest() == e["sha256"], f"{world} rank shares"
+
+
+def test_gpu_scene7_config5_full_size(manifest):
+    """BASELINE config 5 at full size: scene 7 (Book-2 final), 1000x1000, 1000 spp, depth 50."""
+    e = manifest["renders"].get("s7_1000x1000_1000spp_d50")
+    if e is None:
+        pytest.skip("config-5 golden not generated (make_golden.py --big)")
+    img = rtc.render(rtc.Scene.preset(7, 1000, 1000, 50))
+    got = hashlib.sha256(img.tobytes()).hexdigest()
+    if got != e["sha256"]:
+        bad = [c for c, h in e["crops"].items() if hashlib.sha256(
+            img[int(c.split(",")[1]):int(c.split(",")[1]) + 32, int(c.split(",")[0]):int(c.split(",")[0]) + 32]
+            .tobytes()).hexdigest() != h]
+        pytest.fail(f"config-5 full-frame sha mismatch; crops differing: {bad}")
+
+
 @pytest.mark.parametrize("scene,width,spp,depth", [
     (0, 97, 7, 3), (1, 211, 5, 50), (1, 64, 2, 1), (2, 150, 4, 7), (4, 120, 3, 50), (5, 131, 9, 50),
     (6, 90, 6, 50), (7, 128, 4, 50), (3, 100, 3, 2), (1, 2, 11, 50)])
@@ -169,6 +208,13 @@ def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypat
     e = manifest["renders"][name]
     img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), f"{name} {env}")
+
+
+@pytest.mark.parametrize("scene,width,spp,depth", [(1, 96, 6, 65), (1, 80, 4, 100), (5, 64, 4, 100), (7, 48, 2, 120)])
+def test_gpu_depth_beyond_64_matches_oracle(scene, width, spp, depth):
+    """max_depth > 64: the deep kernel (global-memory path records) against the oracle."""
+    sc = rtc.Scene.preset(scene, width, spp, depth)
+    _check(rtc.render(sc), pyoracle.render(sc), f"scene {scene} depth {depth}")
 
 
 def test_book1_deep_paths_spill(monkeypatch):
