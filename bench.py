@@ -3,9 +3,12 @@
 
 Workload (BASELINE.json configs[2]): the Book-1 final scene (reference CLI scene 1, src/main.c:32-85),
 1200x675, 1000 samples per pixel, max depth 50 — exactly `./main 1 1200 1000 _` of the reference.
-A "step" is one full frame: every pixel's 1000-sample path loop, i.e. one kernel launch per GPU
-over that GPU's rows.  The scene arrays are resident in HBM before timing starts; the frame stays
-in HBM (the PCIe-inclusive end-to-end rate of Camera_render is reported separately in DESIGN.md).
+A "step" is one full frame: every pixel's 1000-sample path loop over that GPU's rows -- the launch
+rt_render_rows_async makes (cost pre-pass, device-side plan, chain kernel, fold).  The scene arrays
+are resident in HBM before timing starts; the frame stays in HBM.  At N=1, after timing, rank 0 also
+times the drop-in boundary end to end (rt_render: flatten-free upload, launch, D2H into a host
+buffer, i.e. what Camera_render does after rt_flatten) and reports it as "end_to_end" -- never as
+"value".
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
 GPU, rows j % N == rank, no collective on the data path; the frame is fixed, so this
@@ -32,8 +35,12 @@ sys.path.insert(0, os.path.join(ROOT, "ray-tracing-c_amd"))
 METRIC = "Msamples/s (pixels×spp) Book-1 final 1200×675×1000spp; max-abs pixel diff"
 # FP32 operations per sample (instrumented reference event counts x per-event op counts)
 OPS_PER_SAMPLE = {0: 0.48e3, 1: 2.82e3, 7: 6.0e3}
-PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
-README_M1_MSAMPLES = 5.26     # README.md:43, 2 min 34 s on a MacBook Air M1 (derived)
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate, FMA = 2 flops
+# the realistic ceiling for this code: non-FMA, non-packed VALU issue -- 256 CUs x 4 SIMDs
+# x 32 lanes per cycle (a wave64 VALU op issues over 2 cycles, MI355X_MICROARCH.md) x 2.4 GHz
+ISSUE_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+PMC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_chain.json")
+PMC_CONFIG = "s1_1200x675_1000spp_d50_n1"  # the configuration the committed PMC passes profiled
 
 
 def parse():
@@ -56,7 +63,9 @@ def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle  # test infrastructure: used only as the measured CPU baseline here
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # every hardware thread this process may run on (the reference's OpenMP team default,
+    # src/raytracing.c:91); the cgroup CPU quota, if any, bounds how many of them run at once
+    threads = len(os.sched_getaffinity(0))
     kind, exe = "reference", pyoracle.REF_FAST
     if not os.path.exists(exe):
         return None
@@ -65,11 +74,30 @@ def cpu_baseline(args):
         w, h = pyoracle.ref_render(args.scene, args.width, args.cpu_spp, args.depth, os.path.join(td, "o.rgb"),
                                    fast=True, threads=threads, timeout=600)
         dt = time.perf_counter() - t0
-    return {"value": round(w * h * args.cpu_spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": kind,
+    quota = _cgroup_cpus()
+    cores = min(threads, quota) if quota else threads
+    return {"value": round(w * h * args.cpu_spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": cores,
+            "threads": threads, "cgroup_cpu_quota": quota, "kind": kind,
             "sample": (f"scene {args.scene} {w}x{h} at {args.cpu_spp} spp (of {args.spp}), depth {args.depth}: the "
                        f"reference sources built with its Makefile flags -std=c11 -Ofast -fopenmp "
-                       f"(oracle/_ref/ref_render_fast), {threads} OpenMP threads, wall {dt:.2f} s"),
+                       f"(oracle/_ref/ref_render_fast), {threads} OpenMP threads (sched_getaffinity), "
+                       f"cgroup quota {quota} CPUs, wall {dt:.2f} s"),
             "host_cpu": _cpu_model()}
+
+
+def _cgroup_cpus():
+    """CPUs the cgroup v2 / v1 quota allows (None: unlimited or unknown)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
 
 
 def _cpu_model():
@@ -93,13 +121,17 @@ def golden_for(args):
     return None, None
 
 
-def traffic_for(config_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_traffic.json)."""
+def pmc_for(kernel_name):
+    """The committed rocprofv3 PMC summary of this kernel (scripts/gpu_pmc.sh -> scripts/pmc_summary.py,
+    profiles/r02/pmc_chain.json) for the headline configuration: per-frame HBM bytes and VALU figures."""
     try:
-        t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-        return t.get(config_key, {}).get("hbm_bytes_per_launch")
+        t = json.load(open(PMC_JSON))
     except (OSError, ValueError):
         return None
+    for name, e in t.get("kernels", {}).items():
+        if name.split("(")[0].replace("void ", "").replace(" ", "") == kernel_name.replace(" ", ""):
+            return e
+    return None
 
 
 def main():
@@ -187,7 +219,35 @@ def main():
             name, g = golden_for(args)
             parity = {"frame_sha256": sha, "golden": name,
                       "pixel_identical_to_reference": (sha == g["sha256"]) if g else None,
-                      "max_abs_pixel_diff": 0 if (g and sha == g["sha256"]) else None}
+                      "max_abs_pixel_diff": None}
+            if g and sha == g["sha256"]:
+                parity["max_abs_pixel_diff"] = 0
+            elif g and g.get("file"):  # a full reference image: the actual difference
+                import gzip
+
+                import numpy as np
+                with gzip.open(os.path.join(ROOT, "tests", "golden", g["file"]), "rb") as f:
+                    ref = np.frombuffer(f.read(), np.uint8).reshape(g["height"], g["width"], 3)
+                parity["max_abs_pixel_diff"] = int(np.abs(frame.astype(np.int16) - ref.astype(np.int16)).max())
+            elif g:  # sha and 32x32 crops only: the largest difference inside the differing crops is unknown
+                bad = [c for c, h in g.get("crops", {}).items()
+                       if hashlib.sha256(frame[int(c.split(",")[1]):int(c.split(",")[1]) + 32,
+                                               int(c.split(",")[0]):int(c.split(",")[0]) + 32].tobytes()).hexdigest() != h]
+                parity["crops_differing"] = bad
+
+    # the drop-in boundary end to end (N=1, after timing): rt_render = upload + launch + D2H into a
+    # host buffer, what Camera_render runs after rt_flatten (src/raytracing.c:86-135 as a whole)
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_parity:
+        t_e = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            rtc.render(sc, n_gpus=1)
+            t_e.append(time.perf_counter() - t0)
+        best = min(t_e)
+        e2e = {"value": round(W * H * spp / best / 1e6, 3), "unit": "Msamples/s", "ms": round(best * 1e3, 3),
+               "what": "rt_render (Camera_render after rt_flatten): scene upload, pre-pass, plan, kernels, D2H "
+                       "of the frame into a host buffer; best of 2"}
 
     if rank == 0:
         frame_samples = W * H * spp
@@ -198,6 +258,7 @@ def main():
         workload = (f"Book-1 final scene (reference CLI scene 1) {W}x{H}, {spp} spp, depth {args.depth}"
                     if args.scene == 1 else f"reference scene {args.scene} {W}x{H}, {spp} spp, depth {args.depth}")
         config_key = f"s{args.scene}_{W}x{H}_{spp}spp_d{args.depth}_n{world}"
+        pmc = pmc_for(kernel_name)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -208,26 +269,36 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / README_M1_MSAMPLES, 2) if (args.scene == 1 and W == 1200 and spp == 1000
-                                                                    and args.depth == 50) else None,
-            "vs_baseline_source": "README.md:43 (2 min 34 s, M1, OpenMP) => 5.26 Msamples/s, BASELINE.md",
+            "vs_baseline": round(value / base["value"], 2) if base else None,
+            "vs_baseline_source": ("cpu_baseline below: the reference's own -Ofast OpenMP build on this box's host "
+                                   "cores, same scene and size" if base else "no same-box CPU baseline in this run"),
             "dtype": "f32",
             "data": "synthetic: the reference's procedural scene (pcg32 seed 19,29) and per-pixel pcg32 streams",
             "config": {"workload": workload, "scene": args.scene, "width": W, "height": H, "spp": spp,
                        "max_depth": args.depth, "partition": f"rows j % {world}", "rows_on_rank0": n_rows},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 4) if achieved else None,
+            "roofline": {"bound": "valu", "achieved": round(achieved, 4) if achieved else None,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 5) if achieved else None,
-                         "traffic": traffic_for(config_key),
+                         "issue_ceiling": ISSUE_TOPS,
+                         "frac_of_issue_ceiling": round(achieved / ISSUE_TOPS, 5) if achieved else None,
+                         "traffic": (round(pmc["fetch_bytes"] + pmc["write_bytes"]) if pmc and "fetch_bytes" in pmc
+                                     and "write_bytes" in pmc and config_key == PMC_CONFIG else None),
+                         "pmc": ({k: round(pmc[k], 4) for k in ("valu_busy", "lanes_active", "valu_insts_per_sample",
+                                                                "lds_bank_conflict_frac") if k in pmc}
+                                 if pmc and config_key == PMC_CONFIG else None),
+                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc and config_key == PMC_CONFIG else None,
                          "kernel": kernel_name, "kernel_ms_avg": round(kernel_ms, 3),
                          "step_ms_avg": round(step_ms, 3),
                          "kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
                          "algorithmic_work": f"{ops:.0f} FP32 ops/sample (SURVEY §8d) x {launch_samples} samples/launch"
                          if ops else None,
-                         "note": "compute roof: the dense f32 peak (f32 MFMA rate = FP32 vector rate); the kernel is "
-                                 "branchy FP32 VALU + u64 integer work, no MFMA; the scene sits in LDS, so the HBM roof "
-                                 "does not apply; achieved counts the algorithmic FP32 ops only"},
+                         "note": "VALU-bound branchy FP32 + u64 integer work, no MFMA, scene in LDS (HBM roof does "
+                                 "not apply). peak = dense f32 rate (FMA = 2); issue_ceiling = non-FMA non-packed "
+                                 "VALU lane-ops/s (256 CU x 4 SIMD x 32 lanes x 2.4 GHz), the realistic ceiling for "
+                                 "bit-exact code (no contraction). achieved counts algorithmic FP32 ops only; traffic "
+                                 "= FETCH_SIZE x 2 + WRITE_SIZE bytes per frame from the committed PMC pass"},
             "cpu_baseline": base,
+            "end_to_end": e2e,
             "parity": parity,
         }
         print(json.dumps(line), flush=True)

@@ -6,7 +6,7 @@
  * and re-derives every pixel with the reference's structure: recursive ray colour, recursive
  * hit() over lists / BVH nodes / transforms / media, per-pixel pcg32, glibc libm.
  *
- * Pinning: tests/test_oracle.py checks this restatement against golden renders produced by the
+ * Pinning: tests/test_oracle_golden.py checks this restatement against golden renders produced by the
  * reference's own sources (oracle/_ref, built by oracle/Makefile; fixtures in tests/golden/).
  *
  * Reference citations (ray-tracing-c @ v2):

@@ -1865,6 +1865,10 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
 extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   static thread_local char buf[160];
   if (!d) return "";
+  if (d->deep_rec) {
+    snprintf(buf, sizeof buf, "rt_render_deep_kernel<%d>", (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll);
+    return buf;
+  }
   if (!d->book1) {
     snprintf(buf, sizeof buf, "%s<%d%s>", d->general ? "rt_general_kernel" : "rt_render_rows_kernel",
              (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll,
@@ -1873,9 +1877,9 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   }
   const int mode = pick_mode(d, (int64_t)d->width * d->height);
   const char *lds = d->b1_lds_bytes ? "true" : "false";
-  if (mode == kModeChain) snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s>", lds);
+  if (mode == kModeChain) snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %d>", lds, d->cfg.chain_occ);
   else if (mode == kModeGroup) snprintf(buf, sizeof buf, "rt_book1_group_kernel<%s>", lds);
-  else snprintf(buf, sizeof buf, "rt_book1_kernel<%s>", lds);
+  else snprintf(buf, sizeof buf, "rt_book1_kernel<%s, %d>", lds, d->cfg.lane_occ);
   return buf;
 }
 

@@ -19,8 +19,14 @@
 // s_sinf.c} (ARM optimized-routines).  The FMA placement below is the one gcc emitted for the
 // `*_fma` ifunc variants that glibc selects on FMA-capable x86-64 (read off the disassembly of
 // /lib/x86_64-linux-gnu/libm.so.6, glibc 2.35-0ubuntu3.11); the table words were read from the
-// same library (oracle/tools/extract_libm_tables.c).  tests/test_libm_port.py checks every port
-// against the host libm over the full domain the hot path can feed it.
+// same library: oracle/tools/extract_libm_tables.cpp locates every table there and checks it word
+// for word against this file (tests/test_libm_port.py runs it).  tests/test_libm_port.py also checks
+// every port against the host libm over the full domain the hot path can feed it.
+//
+// Licence: the algorithms, polynomial coefficients and tables below are glibc's, a derived work
+// under the GNU Lesser General Public License v2.1 or later (sincosf / powf / logf: ARM
+// optimized-routines, Copyright (c) 2017-2018 Arm Ltd; atanf / acosf: fdlibm, Copyright (C) 1993
+// Sun Microsystems).  See THIRD_PARTY.md.
 //
 // Compile with -ffp-contract=off: every fused multiply-add below is an explicit fma().
 #pragma once

@@ -30,6 +30,16 @@ def test_port_exhaustive_on_host(fn):
     assert r.returncode == 0 and " mismatches=0 " in r.stdout, r.stdout + r.stderr
 
 
+def test_port_tables_are_the_host_libm_words():
+    """Provenance of the port's tables: oracle/tools/extract_libm_tables.cpp finds every table in the
+    host libm.so.6 (the library the reference links) and compares it word for word with rt_libm.h."""
+    exe = os.path.join(BIN, "extract_libm_tables")
+    if not os.path.exists("/lib/x86_64-linux-gnu/libm.so.6"):
+        pytest.skip("no x86-64 glibc libm here")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "all tables identical to the host libm" in r.stdout, r.stdout + r.stderr
+
+
 def test_port_sincos_large_arguments_sample_on_host():
     """|x| >= 120 uses the 4/pi bit-table reduction (Perlin's sinf argument can get there)."""
     lo, hi = 0x42f00000, 0x42f00000 + (1 << 22)
