@@ -63,9 +63,12 @@ def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle  # test infrastructure: used only as the measured CPU baseline here
 
-    # every hardware thread this process may run on (the reference's OpenMP team default,
-    # src/raytracing.c:91); the cgroup CPU quota, if any, bounds how many of them run at once
-    threads = len(os.sched_getaffinity(0))
+    # the reference's OpenMP team default is every hardware thread (src/raytracing.c:91); here that is
+    # every CPU this process may run on, capped by the cgroup CPU quota when one is set (the GPU box
+    # grants 16 CPUs of a 128-core host: 256 threads under a 16-CPU quota measured 20x slower)
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    threads = min(affinity, max(1, int(quota + 0.5))) if quota else affinity
     kind, exe = "reference", pyoracle.REF_FAST
     if not os.path.exists(exe):
         return None
@@ -74,14 +77,12 @@ def cpu_baseline(args):
         w, h = pyoracle.ref_render(args.scene, args.width, args.cpu_spp, args.depth, os.path.join(td, "o.rgb"),
                                    fast=True, threads=threads, timeout=600)
         dt = time.perf_counter() - t0
-    quota = _cgroup_cpus()
-    cores = min(threads, quota) if quota else threads
-    return {"value": round(w * h * args.cpu_spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": cores,
-            "threads": threads, "cgroup_cpu_quota": quota, "kind": kind,
+    return {"value": round(w * h * args.cpu_spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
+            "threads": threads, "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "kind": kind,
             "sample": (f"scene {args.scene} {w}x{h} at {args.cpu_spp} spp (of {args.spp}), depth {args.depth}: the "
                        f"reference sources built with its Makefile flags -std=c11 -Ofast -fopenmp "
-                       f"(oracle/_ref/ref_render_fast), {threads} OpenMP threads (sched_getaffinity), "
-                       f"cgroup quota {quota} CPUs, wall {dt:.2f} s"),
+                       f"(oracle/_ref/ref_render_fast), {threads} OpenMP threads = the {affinity} affine CPUs "
+                       f"capped by the cgroup quota ({quota} CPUs), wall {dt:.2f} s"),
             "host_cpu": _cpu_model()}
 
 
