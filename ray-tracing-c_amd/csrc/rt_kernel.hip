@@ -126,8 +126,13 @@ __global__ __launch_bounds__(256) void chain_fold_kernel(b1::Book1View V, uint8_
 }
 
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
-template <int F, bool kBatch = false>
-__global__ __launch_bounds__(gen::kBlock, kBatch ? 3 : 1) void rt_general_kernel(gen::GeneralView V, uint8_t *__restrict__ out) {
+// kThreads = kBigBlock: one 768-thread workgroup per CU (3 waves per SIMD, as the 256-thread variant
+// at occupancy 3) holding the scene's WHOLE preorder in LDS (up to 160 KiB per workgroup on gfx950;
+// scene 7's 4946 entries are 158 KiB), so no traversal step waits on L2.
+constexpr int kBigBlock = 768;
+template <int F, bool kBatch = false, int kThreads = gen::kBlock>
+__global__ __launch_bounds__(kThreads, kThreads == gen::kBlock ? (kBatch ? 3 : 1) : 1) void rt_general_kernel(
+    gen::GeneralView V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   gen::render_general<F, kBatch>(V, out, (float4 *)lds);
 }
@@ -588,6 +593,7 @@ struct Config {
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
   int gen_batch = 56, gen_steps = 8, gen_lds = 1024;
+  bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
@@ -647,6 +653,7 @@ struct Config {
     c.gen_batch = env_int("RT_GEN_BATCH", 56);
     c.gen_batch = c.gen_batch < 0 ? 0 : (c.gen_batch > 64 ? 64 : c.gen_batch);
     c.gen_lds = env_int("RT_GEN_LDS", 1024);
+    c.gen_big = env_flag("RT_GEN_BIG", true);
     c.gen_steps = env_int("RT_GEN_STEPS", 8);
     if (c.gen_steps < 1) c.gen_steps = 1;
     return c;
@@ -700,7 +707,7 @@ struct rt_device_scene {
   bool general = false;
   void *gen_arena = nullptr;
   int32_t *gen_counter = nullptr;
-  int gen_grid = 0;
+  int gen_grid = 0, gen_block = 256;
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_lds = 0;
 };
@@ -1155,18 +1162,30 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   int lds = batch ? cfg.gen_lds : 0;
   if (lds < 0) lds = 0;
   if (lds > d->view.n_pre) lds = d->view.n_pre;
-  if (lds > 2048) lds = 2048;  // 64 KB: the default dynamic LDS limit
-  d->gen_lds = lds;
+  if (lds > 2048) lds = 2048;  // 64 KB per 256-thread workgroup (three per CU)
   const bool fb = (d->features & ~kFeatBook1) == 0;
-  const void *fn = batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
+  const size_t pre_bytes = (size_t)d->view.n_pre * 2 * sizeof(float4);
+  d->gen_block = gen::kBlock;
+  if (batch && cfg.gen_big && d->view.n_pre > lds && pre_bytes <= (size_t)prop.sharedMemPerBlock) {
+    d->gen_block = kBigBlock;  // the whole preorder in one workgroup's LDS
+    lds = d->view.n_pre;
+  }
+  d->gen_lds = lds;
+  const bool big = d->gen_block == kBigBlock;
+  const void *fn = big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
+                             : (const void *)rt_general_kernel<kFeatAll, true, kBigBlock>)
+                 : batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
                          : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
+  const size_t lds_bytes = (size_t)lds * 2 * sizeof(float4);
+  if (lds_bytes > 65536) HIP_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
   int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gen::kBlock, (size_t)lds * 2 * sizeof(float4)));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, d->gen_block, lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->gen_grid = prop.multiProcessorCount * per_cu;
   d->general = true;
   if (cfg.debug)
-    fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU), features=0x%x\n", d->gen_grid, per_cu, d->features);
+    fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, features=0x%x\n",
+            d->gen_grid, per_cu, d->gen_block, d->gen_lds, d->view.n_pre, d->features);
   return 0;
 }
 
@@ -1570,6 +1589,12 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.steps = d->cfg.gen_steps;
   V.n_lds = d->gen_lds;
   const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
+  if (V.batch && d->gen_block == kBigBlock) {
+    const dim3 bb(kBigBlock);
+    if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, kBigBlock>), g, bb, lds_bytes, st, V, d_out);
+    else hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true, kBigBlock>), g, bb, lds_bytes, st, V, d_out);
+    return;
+  }
   if (all && V.batch)
     hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true>), g, b, lds_bytes, st, V, d_out);
   else if (all)
@@ -1630,7 +1655,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
       LptModel model;
       model.spp_ratio = 1.0f;
-      model.grid_waves = d->gen_grid * (gen::kBlock / 64);
+      model.grid_waves = d->gen_grid * (d->gen_block / 64);
       model.lat_step = kLaneLat;
       model.thr_step = kLaneThr;
       model.coop_step = kCoopStep;
@@ -1872,7 +1897,8 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   if (!d->book1) {
     snprintf(buf, sizeof buf, "%s<%d%s>", d->general ? "rt_general_kernel" : "rt_render_rows_kernel",
              (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll,
-             d->general && d->view.pre && d->cfg.gen_batch ? ", true" : d->general ? ", false" : "");
+             d->general && d->gen_block == kBigBlock ? ", true, 768"
+             : d->general && d->view.pre && d->cfg.gen_batch ? ", true" : d->general ? ", false" : "");
     return buf;
   }
   const int mode = pick_mode(d, (int64_t)d->width * d->height);
