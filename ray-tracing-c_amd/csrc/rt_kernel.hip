@@ -584,7 +584,7 @@ enum : int { kModeLane = 0, kModeGroup = 1, kModeChain = 2, kModeAuto = 3 };
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
   bool lpt = true, bf = true, coop_sort = true, wave_prio = true, px_time = false, debug = false;
-  int lpt_spp = 8, coop_steps = -1, coop_waves = -1, shade_batch = 48;
+  int lpt_spp = 16, coop_steps = -1, coop_waves = -1, shade_batch = 48;
   int mode = kModeAuto;
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
@@ -622,7 +622,7 @@ struct Config {
     c.wave_prio = env_flag("RT_WAVE_PRIO", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
-    c.lpt_spp = env_int("RT_LPT_SPP", 8);
+    c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
     if (c.lpt_spp < 1) c.lpt_spp = 1;
     c.coop_steps = env_int("RT_COOP_STEPS", -1);
     c.coop_waves = env_int("RT_COOP_WAVES", -1);
