@@ -819,7 +819,7 @@ RT_D float lights_pdf(const DScene &S, f3 o, f3 d) {
 // Paths longer than kMaxDepth (kDeep): the record lives in a caller-provided global-memory slot of
 // max_depth entries instead of registers / scratch (rt_render_deep_kernel).
 struct DeepRec {
-  f3 a, e;
+  f3 a;
   float w;
   uint32_t weighted;
 };
@@ -827,8 +827,9 @@ struct DeepRec {
 template <int F, bool kDeep = false>
 RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g, DeepRec *deep = nullptr) {
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
+  // a recorded (scattering) bounce's emission is always +0: only SurfaceNormal and DiffuseLight emit
+  // and neither scatters (src/material.c:103-142); the fold adds that +0 as the reference does
   f3 rec_a[kDeep ? 1 : kMaxDepth];
-  f3 rec_e[kFull && !kDeep ? kMaxDepth : 1];
   float rec_w[kFull && !kDeep ? kMaxDepth : 1];
   uint64_t weighted = 0;
   int n = 0;
@@ -856,8 +857,6 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g, DeepRec *deep = nullpt
     if (kDeep) deep[n].a = albedo, deep[n].weighted = 0u;
     else rec_a[n] = albedo;
     if (kFull) {
-      if (kDeep) deep[n].e = e;
-      else rec_e[n] = e;
       // mixture pdf (src/raytracing.c:56-71): only when the scene has lights and p != 0 (runtime bit:
       // a kernel variant compiled with the LIGHTS path may run a scene without lights)
       if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
@@ -880,12 +879,9 @@ RT_D f3 path_color(const DScene &S, f3 o, f3 d, Pcg32 &g, DeepRec *deep = nullpt
   f3 c = tail;
   for (int k = n - 1; k >= 0; k--) {
     f3 x = mul(kDeep ? deep[k].a : rec_a[k], c);
-    if (kFull) {
-      if (kDeep ? deep[k].weighted != 0u : ((weighted >> k) & 1) != 0) x = scale(x, kDeep ? deep[k].w : rec_w[k]);
-      c = add(kDeep ? deep[k].e : rec_e[k], x);
-    } else {
-      c = add(mk(0.0f, 0.0f, 0.0f), x);
-    }
+    if (kFull && (kDeep ? deep[k].weighted != 0u : ((weighted >> k) & 1) != 0))
+      x = scale(x, kDeep ? deep[k].w : rec_w[k]);
+    c = add(mk(0.0f, 0.0f, 0.0f), x);
   }
   return c;
 }

@@ -45,9 +45,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   const float prob = S.cam.light_prob;
   const int spp = S.cam.spp;
 
-  // per-lane path state (path_color's locals, kept across iterations)
+  // per-lane path state (path_color's locals, kept across iterations).  A recorded bounce's
+  // emission is always +0 (only SurfaceNormal and DiffuseLight emit, and neither scatters:
+  // src/material.c:103-142), so the record is (albedo, pdf weight) and the fold adds +0 as the
+  // reference's vec3_add(emission_color, scatter_color) does.
   f3 rec_a[kMaxDepth];
-  f3 rec_e[kFull ? kMaxDepth : 1];
   float rec_w[kFull ? kMaxDepth : 1];
   uint64_t weighted = 0;
   int n = 0, depth = 0, s = 0, i = 0, j = 0;
@@ -170,7 +172,6 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         } else {
           rec_a[n] = albedo;
           if (kFull) {
-            rec_e[n] = e;
             if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
               if (g.f32() < prob) dir = lights_rand(S, r.p, g);
               const float sp = scatter_pdf(S, r.material, r.normal, dir);
@@ -197,12 +198,8 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     f3 c = tail;
     for (int k = n - 1; k >= 0; k--) {
       f3 x = mul(rec_a[k], c);
-      if (kFull) {
-        if ((weighted >> k) & 1) x = scale(x, rec_w[k]);
-        c = add(rec_e[k], x);
-      } else {
-        c = add(mk(0.0f, 0.0f, 0.0f), x);
-      }
+      if (kFull && ((weighted >> k) & 1)) x = scale(x, rec_w[k]);
+      c = add(mk(0.0f, 0.0f, 0.0f), x);
     }
     acc = add(acc, c);
     s++;

@@ -21,7 +21,7 @@ from . import earth
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # ray-tracing-c_amd/
 # RTC_LIB: an alternative build of the same library (same-box A/B timing of two builds; tests and
 # bench use the in-tree library)
-LIB_PATH = os.environ.get("RTC_LIB") or os.path.join(PKG_DIR, "librtc_amd.so")
+LIB_PATH = os.path.abspath(os.environ.get("RTC_LIB") or os.path.join(PKG_DIR, "librtc_amd.so"))
 
 # rt_feature_bits (include/rt_flat.h)
 FEAT_BVH, FEAT_QUAD, FEAT_XFORM, FEAT_MEDIUM = 1, 2, 4, 8
