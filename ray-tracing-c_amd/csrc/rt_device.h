@@ -376,7 +376,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
 // 2 float4, so trace_pre is a scan with skips, without a stack:
 //   BVH node:   q0 = (lo.x, lo.y, lo.z, hi.x)  q1 = (hi.y, hi.z, skip, ref)  next = hit ? p+1 : skip
 //   transform:  q0 = (end, -, enclosing transform's position or ~0, -)  q1 = (-, -, end, ref)
-//   sphere:     q0 = (center, r^2); quad: q0 = (normal, D); medium: -; q1.w = ref     next = p+1
+//   sphere:     q0 = (center, r^2); quad: q0 = (normal, D); q1.w = ref                 next = p+1
+//   medium:     sphere boundary: q0 = its (center, r^2), q1 = (-1/density, 1 (bits), -, ref); else -
 // (skip / end = the position after the subtree; integers stored as float bits).  Lists need no
 // entry.  Visit order, frames, t_max and rng draws (media) are the stack machine's.
 // The scan's state, so that a caller can run it a few entries at a time (rt_general.h).
@@ -460,18 +461,32 @@ RT_D bool pre_step(const DScene &S, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32
     T.inv = mk(1.0f / T.d.x, 1.0f / T.d.y, 1.0f / T.d.z);
     T.dd = dot(T.d, T.d);
   } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
-    // ConstantMedium_hit (src/hittable.c:392-423): two boundary hits, clamp, one rng draw
-    const rt_medium m = S.media[idx];
-    float t1, t2;
-    if (prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
-        prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2)) {
+    // ConstantMedium_hit (src/hittable.c:392-423): two boundary hits, clamp, one rng draw.  A
+    // sphere boundary's centre / r^2 and the density sit in the entry (no dependent loads).
+    const bool inl = __builtin_bit_cast(uint32_t, q1.y) == 1u;
+    float t1, t2, nid;
+    bool both;
+    if (inl) {
+      rt_sphere sp;
+      sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
+      const float a = dot(d, d);
+      both = sphere_t(sp, o, d, a, -__builtin_inff(), __builtin_inff(), t1) &&
+             sphere_t(sp, o, d, a, t1 + 0.0001f, __builtin_inff(), t2);
+      nid = q1.x;
+    } else {
+      const rt_medium m = S.media[idx];
+      both = prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
+             prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2);
+      nid = m.neg_inv_density;
+    }
+    if (both) {
       t1 = fmaxf(t1, tmin);
       t2 = fminf(t2, T.tmax);
       if (!(t1 >= t2)) {
         t1 = t1 > 0.0f ? t1 : 0.0f;
         const float len = sqrtf(T.dd);
         const float inside = (t2 - t1) * len;
-        const float dist = m.neg_inv_density * rtm::logf(g.f32());
+        const float dist = nid * rtm::logf(g.f32());
         if (!(dist > inside)) {
           t = t1 + dist / len;
           hit = true;
@@ -528,8 +543,15 @@ struct PreorderBuilder {
       const rt_quad &qd = s.quads[idx];
       q0 = make_float4(qd.normal[0], qd.normal[1], qd.normal[2], qd.D);
     }
+    float4 q1 = make_float4(0.0f, 0.0f, 0.0f, b((uint32_t)ref));
+    if (kind == RT_KIND_MEDIUM && rt_ref_kind(s.media[idx].boundary) == RT_KIND_SPHERE) {  // boundary inline
+      const rt_sphere &sp = s.spheres[rt_ref_index(s.media[idx].boundary)];
+      q0 = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius_sq);
+      q1.x = s.media[idx].neg_inv_density;
+      q1.y = b(1u);
+    }
     out.push_back(q0);
-    out.push_back(make_float4(0.0f, 0.0f, 0.0f, b((uint32_t)ref)));
+    out.push_back(q1);
     if (kind == RT_KIND_BVH) {
       const rt_bvh_node &nd = s.bvh[idx];
       emit(nd.left, enclosing);
