@@ -594,6 +594,7 @@ struct Config {
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
   int gen_batch = 56, gen_steps = 8, gen_lds = 1024;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
+  int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
@@ -654,6 +655,7 @@ struct Config {
     c.gen_batch = c.gen_batch < 0 ? 0 : (c.gen_batch > 64 ? 64 : c.gen_batch);
     c.gen_lds = env_int("RT_GEN_LDS", 1024);
     c.gen_big = env_flag("RT_GEN_BIG", true);
+    c.gen_big_block = env_int("RT_GEN_BIG_BLOCK", c.gen_big_block);
     c.gen_steps = env_int("RT_GEN_STEPS", 8);
     if (c.gen_steps < 1) c.gen_steps = 1;
     return c;
@@ -1167,12 +1169,14 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const size_t pre_bytes = (size_t)d->view.n_pre * 2 * sizeof(float4);
   d->gen_block = gen::kBlock;
   if (batch && cfg.gen_big && d->view.n_pre > lds && pre_bytes <= (size_t)prop.sharedMemPerBlock) {
-    d->gen_block = kBigBlock;  // the whole preorder in one workgroup's LDS
+    d->gen_block = cfg.gen_big_block == 1024 ? 1024 : kBigBlock;  // the whole preorder in one workgroup's LDS
     lds = d->view.n_pre;
   }
   d->gen_lds = lds;
-  const bool big = d->gen_block == kBigBlock;
-  const void *fn = big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
+  const bool big = d->gen_block == kBigBlock, big4 = d->gen_block == 1024;
+  const void *fn = big4 ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, 1024>
+                              : (const void *)rt_general_kernel<kFeatAll, true, 1024>)
+                 : big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
                              : (const void *)rt_general_kernel<kFeatAll, true, kBigBlock>)
                  : batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
                          : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
@@ -1589,6 +1593,12 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.steps = d->cfg.gen_steps;
   V.n_lds = d->gen_lds;
   const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
+  if (V.batch && d->gen_block == 1024) {
+    const dim3 bb(1024);
+    if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, 1024>), g, bb, lds_bytes, st, V, d_out);
+    else hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true, 1024>), g, bb, lds_bytes, st, V, d_out);
+    return;
+  }
   if (V.batch && d->gen_block == kBigBlock) {
     const dim3 bb(kBigBlock);
     if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, kBigBlock>), g, bb, lds_bytes, st, V, d_out);
@@ -1897,7 +1907,7 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   if (!d->book1) {
     snprintf(buf, sizeof buf, "%s<%d%s>", d->general ? "rt_general_kernel" : "rt_render_rows_kernel",
              (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll,
-             d->general && d->gen_block == kBigBlock ? ", true, 768"
+             d->general && d->gen_block == 1024 ? ", true, 1024" : d->general && d->gen_block == kBigBlock ? ", true, 768"
              : d->general && d->view.pre && d->cfg.gen_batch ? ", true" : d->general ? ", false" : "");
     return buf;
   }
