@@ -374,7 +374,7 @@ __global__ __launch_bounds__(1024) void lpt_coop_sort_kernel(const uint32_t *cos
 enum : int {
   kCnItems = 0, kCnSplit = 1, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
   kCnCoopWaves = 7, kCnCoopCounter = 8, kCnNCoop = 9, kCnWaveWork = 10 /* u64 */, kCnCstar = 12, kCnCstarW = 13,
-  kCnHist = 256, kCnOff = 512, kCnWords = 1024
+  kCnHist = 256, kCnOff = 512, kCnCstarTab = 768, kCnWords = 1024
 };
 
 struct ChainModel {
@@ -382,6 +382,7 @@ struct ChainModel {
   int grid_waves;       // waves of the lane kernel's grid
   float lat, thr, coop; // clocks per pre-pass step: lane chain latency, per-lane throughput, whole wave
   float beta;           // a lane chain's latency target, as a fraction of the launch's throughput time
+  float floor_beta;     // > 0: per cost bucket, the time left after the heavier buckets (chain_params_kernel)
   float margin;         // records per segment: margin * spp / K + slack
   int slack;
   int kmax_lane, kmax_wave;
@@ -401,6 +402,16 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
   const float cstar = (float)fmax(1.0, m.beta * total * m.thr / (lanes * m.lat));
   cnt[kCnCstar] = __float_as_uint(cstar);
   cnt[kCnCstarW] = __float_as_uint(cstar * m.lat / m.coop);
+  // per cost bucket: lanes take pixels heaviest first, so a pixel of bucket b starts once the work
+  // of the heavier buckets is done (t_b = W_above(b) / throughput) and has T - t_b left before the
+  // launch's throughput time T: its chains get that slack, not T (floor: m.floor_beta * T)
+  double above = 0.0;
+  for (int b = 255; b >= 0; b--) {
+    const double left = fmax(m.beta * (total - above), m.floor_beta * total);
+    const float cb = m.floor_beta > 0.0f ? (float)fmax(1.0, left * m.thr / (lanes * m.lat)) : cstar;
+    cnt[kCnCstarTab + b] = __float_as_uint(cb);
+    above += (double)sums[b];
+  }
 }
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
@@ -411,9 +422,10 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
   for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
   if (threadIdx.x == 0) wwork = 0;
   __syncthreads();
-  const float cstar = __uint_as_float(cnt[kCnCstar]), cstar_w = __uint_as_float(cnt[kCnCstarW]);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     const uint32_t c = cost[p];
+    const float cstar = __uint_as_float(cnt[kCnCstarTab + lpt_bucket(c)]);
+    const float cstar_w = cstar * m.lat / m.coop;
     int K = (int)fminf(ceilf((float)c / cstar), 1e6f);
     bool wave = false;
     if (K > m.kmax_lane && m.kmax_wave > 0) {  // too long for lane chains: whole-wave chains
@@ -589,6 +601,7 @@ struct Config {
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
+  float chain_floor = 0.0f;  // > 0: per-bucket chain targets (measured: N=2/4 +2-5 %, N=1/8 -7 %; off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
@@ -647,6 +660,7 @@ struct Config {
     c.chain_smooth = env_int("RT_CHAIN_SMOOTH", c.chain_smooth);
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
+    c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
     if (const char *e = getenv("RT_MODEL_LANE")) sscanf(e, "%f,%f,%f", &c.lane_lat, &c.lane_thr, &c.lane_coop);
@@ -1398,6 +1412,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.thr = cfg.lane_thr;
   m.coop = cfg.lane_coop;
   m.beta = cfg.chain_beta;
+  m.floor_beta = cfg.chain_floor;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
   m.width = V.S.cam.width;
