@@ -157,6 +157,7 @@ struct Book1View {
   uint32_t mig_epoch;  // per launch (> 0): marks the queue entries this launch wrote
   int32_t mig_idle;    // migrate only once more waves than this have become helpers
   int32_t mig_sleep;     // helpers poll their mailbox every mig_sleep * ~3.4 us
+  unsigned long long *loop_stats;  // diagnostic builds (-DRT_LOOP_STATS): per-launch loop counters
   int32_t mig_max_help;  // at most this many finished waves stay as helpers; the others leave.  Resident
                          // idle waves slow the working ones (measured: all 5120 waves of a grid kept
                          // resident made N = 8 shares 20 % slower, however rarely they polled)
@@ -976,6 +977,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const float tmin = 1e-3f;
 
   int mode = kWait;
+#ifdef RT_LOOP_STATS
+  uint64_t st_cyc[2] = {0, 0}, st_last = 0, st_it[2] = {0, 0}, st_lanes[2] = {0, 0}, st_live = 0;
+  int st_kind = 0;
+#endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
   uint64_t mig_next = 0;
   bool have_result = false;  // false: this lane first needs a work item
@@ -1014,6 +1019,17 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     const int live = (int)__popcll(trav | wait);
     const int batch = min(V.shade_batch, (3 * live + 3) / 4);
     const bool do_trav = trav != 0 && (int)__popcll(wait) < batch;
+#ifdef RT_LOOP_STATS
+    {  // per wave: iterations, lanes, clocks of traversal vs shading passes
+      const uint64_t now = clock64();
+      if (st_last) st_cyc[st_kind] += now - st_last;
+      st_last = now;
+      st_kind = do_trav ? 0 : 1;
+      st_it[st_kind]++;
+      st_lanes[st_kind] += (uint32_t)__popcll(do_trav ? trav : wait);
+      st_live += (uint32_t)live;
+    }
+#endif
     if (do_trav) {
       // ---------------- traversal steps for every lane still traversing
       if (mode == kTrav) {
@@ -1188,6 +1204,19 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     have_result = true;
     mode = V.n_items9 > 0 ? kTrav : kWait;
   }
+#ifdef RT_LOOP_STATS
+  if (V.loop_stats && __lane_id() == 0) {
+    if (st_last) st_cyc[st_kind] += clock64() - st_last;
+    unsigned long long *o = V.loop_stats + 8 * kMode;
+    atomicAdd(o + 0, (unsigned long long)st_it[0]);
+    atomicAdd(o + 1, (unsigned long long)st_lanes[0]);
+    atomicAdd(o + 2, (unsigned long long)st_cyc[0]);
+    atomicAdd(o + 3, (unsigned long long)st_it[1]);
+    atomicAdd(o + 4, (unsigned long long)st_lanes[1]);
+    atomicAdd(o + 5, (unsigned long long)st_cyc[1]);
+    atomicAdd(o + 6, (unsigned long long)st_live);
+  }
+#endif
   if (kMode == kMigMode && V.mig_live > 0) {
     // (not inlined, so that the whole-wave code does not enlarge the lane loop's register budget;
     // the view is passed as its kernel argument's address -- V is the kernels' first argument --

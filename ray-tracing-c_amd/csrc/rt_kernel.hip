@@ -1121,6 +1121,10 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     HIP_OK(hipMalloc(&d->px_time, npix * 2 * sizeof(uint32_t)));
     V.px_time = d->px_time;
   }
+#ifdef RT_LOOP_STATS
+  HIP_OK(hipMalloc(&V.loop_stats, 32 * sizeof(unsigned long long)));
+  HIP_OK(hipMemset(V.loop_stats, 0, 32 * sizeof(unsigned long long)));
+#endif
   // chain scratch for the whole frame (a launch covers at most every pixel)
   {
     const int kmax = cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave;
@@ -1508,6 +1512,18 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
     HIP_OK(hipEventElapsedTime(&t_cont, dbg_ev[1], dbg_ev[2]));
     for (auto &e : dbg_ev) HIP_OK(hipEventDestroy(e));
     fprintf(stderr, "[rtc] chain launch ms: chains %.2f fold %.2f continuations %.2f\n", t_chains, t_fold, t_cont);
+#ifdef RT_LOOP_STATS
+    {  // cumulative over the scene's launches; kMode 2 row
+      unsigned long long q[32];
+      HIP_OK(hipMemcpy(q, V.loop_stats, sizeof q, hipMemcpyDeviceToHost));
+      const unsigned long long *r = q + 16;
+      const double cyc = (double)(r[2] + r[5]);
+      fprintf(stderr, "[rtc] loop stats (cumulative): trav iters %llu lanes/iter %.1f cycles %.1f%% | shade passes %llu "
+              "lanes/pass %.1f cycles %.1f%% | live lanes/iter %.1f\n", r[0], r[0] ? (double)r[1] / r[0] : 0.0,
+              100.0 * r[2] / cyc, r[3], r[3] ? (double)r[4] / r[3] : 0.0, 100.0 * r[5] / cyc,
+              (r[0] + r[3]) ? (double)r[6] / (r[0] + r[3]) : 0.0);
+    }
+#endif
 
     uint32_t c[16];
     HIP_OK(hipStreamSynchronize(st));
