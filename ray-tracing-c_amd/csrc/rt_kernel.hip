@@ -98,8 +98,8 @@ __global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_chain_kernel(b1::Bo
   b1::render_batched<kLds, 2>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
-template <bool kLds>
-__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 1>(V, out, lds);
 }
@@ -1337,6 +1337,13 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.order = nullptr;
   P.n_coop = nullptr;
+  // at the chain kernel's occupancy (4: no spills) on its grid, else the lane kernel's
+  if (d->cfg.chain_occ == 4) {
+    const dim3 g4((unsigned)d->chain_grid), blk(b1::kBlock);
+    if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true, 4>), g4, blk, d->b1_lds_bytes, st, P, d_out);
+    else hipLaunchKernelGGL((rt_book1_cost_kernel<false, 4>), g4, blk, 0, st, P, d_out);
+    return;
+  }
   const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
   if (d->b1_lds_bytes)
     hipLaunchKernelGGL((rt_book1_cost_kernel<true>), g1, blk, d->b1_lds_bytes, st, P, d_out);
