@@ -126,6 +126,7 @@ struct Book1View {
   const int32_t *order;      // work item order (longest-first from the cost pre-pass), or null
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
+  uint32_t sample_cost;      // cost pre-pass: traversal-step equivalent of one sample's fixed latency
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // the first *n_coop items (of `order` / ch_items) go to whole waves
   int32_t *coop_counter;     //   (render_pixel_coop), claimed through this counter
@@ -1094,7 +1095,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          if (kMode == 1) V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
+          // (+ a per-sample constant: a sample's latency is ~sample_cost traversal steps beyond its own
+          // steps -- camera ray, shading passes, batch waits; fitted on chain timelines)
+          if (kMode == 1)
+            V.cost_out[pix] = (cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps) + V.sample_cost * (uint32_t)spp;
           if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);

@@ -614,6 +614,7 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
   int lane_occ = 5;   // lane kernel occupancy target
+  int sample_cost = 0;     // cost pre-pass: per-sample latency in traversal steps (measured: 75-250 slower; off)
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   static Config from_env() {
     Config c;
@@ -621,6 +622,8 @@ struct Config {
     c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ) == 5 ? 5 : 4;
     c.lane_occ = env_int("RT_LANE_OCC", c.lane_occ) == 4 ? 4 : 5;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
+    c.sample_cost = env_int("RT_SAMPLE_COST", c.sample_cost);
+    if (c.sample_cost < 0) c.sample_cost = 0;
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -1335,6 +1338,7 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.cost_out = d->lpt_cost;
   P.draw_out = d->draw_out;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
+  P.sample_cost = (uint32_t)d->cfg.sample_cost;
   P.order = nullptr;
   P.n_coop = nullptr;
   // at the chain kernel's occupancy (4: no spills) on its grid, else the lane kernel's
@@ -1902,8 +1906,9 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   std::vector<uint2> items(n_items);
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg(n_seg);
-  std::vector<uint32_t> pt(2 * npix), sgt(2 * n_seg), draws(npix);
+  std::vector<uint32_t> pt(2 * npix), sgt(2 * n_seg), draws(npix), costs(npix);
   HIP_OK(hipMemcpy(draws.data(), d->draw_out, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(costs.data(), d->lpt_cost, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(items.data(), d->ch_items, n_items * sizeof(uint2), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(px.data(), d->ch_px, npix * sizeof(b1::ChainPx), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(seg.data(), d->ch_seg, n_seg * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1912,11 +1917,13 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   const uint32_t spp = (uint32_t)d->view.cam.spp;
   for (size_t k = 0; k < n_items && (int64_t)k < max_rows; k++) {
     const uint32_t p = items[k].x, sg = items[k].y;
-    uint32_t *r = rows + 12 * k;
+    uint32_t *r = rows + 16 * k;
     r[0] = p;
     r[3] = k < c[kCnNCoop] ? 1u : 0u;
     r[8] = r[9] = r[10] = 0u;
     r[11] = draws[p];
+    r[12] = costs[p];
+    r[13] = r[14] = r[15] = 0u;
     if (sg & b1::kItemUnsplit) {
       r[1] = 0, r[2] = 1, r[4] = pt[2 * p], r[5] = pt[2 * p + 1], r[6] = spp, r[7] = 2u;
     } else {

@@ -28,7 +28,7 @@ L = rtc.lib()
 L.rt_scene_chain_diag.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
 L.rt_scene_chain_diag.restype = ctypes.c_int64
 cap = sc.width * sc.height * 64
-rows = np.zeros((cap, 12), np.uint32)
+rows = np.zeros((cap, 16), np.uint32)
 m = L.rt_scene_chain_diag(ds._h, rows.ctypes.data, cap)
 assert m >= 0, rtc.last_error()
 r = rows[:m].astype(np.int64)
@@ -74,4 +74,7 @@ last = np.argsort(-end)[:16]
 print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, flags, link t:c, seg_len, pre-pass draws)")
 for q in last:
     print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]} {r[q, 8]}:{r[q, 9]} {r[q, 10]} {r[q, 11]}")
+if os.environ.get("CHAIN_ROWS"):  # the item rows for offline analysis (uint32, compressed)
+    np.savez_compressed(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", f"chain_rows_{world}_{rank}.npz"),
+                        rows=rows[:m])
 ds.close()
