@@ -386,6 +386,7 @@ struct ChainModel {
   float margin;         // records per segment: margin * spp / K + slack
   int slack;
   int kmax_lane, kmax_wave;
+  int kmin;             // every lane pixel gets at least this many segments (launches with few pixels)
   int spp;
   int min_seg;          // samples per segment at least
   int width, smooth;    // launch row width; draw estimates averaged over +-smooth pixels of the row
@@ -432,6 +433,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       wave = true;
       K = min((int)fminf(ceilf((float)c / cstar_w), 1e6f), m.kmax_wave);
     }
+    if (!wave && K < m.kmin) K = m.kmin;  // fill: at least kmin segments when pixels are fewer than lanes
     K = min(K, max(m.kmax_lane, m.kmax_wave));  // (the item and end-word arrays are sized for this)
     K = max(1, min(K, m.spp / m.min_seg));
     // the stream's length at full spp: the pre-pass draws per sample, averaged over the pixel's row
@@ -601,6 +603,7 @@ struct Config {
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
+  float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
   float chain_floor = 0.0f;  // > 0: per-bucket chain targets (measured: N=2/4 +2-5 %, N=1/8 -7 %; off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
@@ -664,6 +667,7 @@ struct Config {
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
     c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
+    c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
     if (const char *e = getenv("RT_MODEL_LANE")) sscanf(e, "%f,%f,%f", &c.lane_lat, &c.lane_thr, &c.lane_coop);
@@ -1434,6 +1438,12 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.smooth = cfg.chain_smooth;
   m.est_scale = cfg.chain_est;
   m.kmax_lane = cfg.chain_kmax;
+  {  // enough items to give every lane of the grid one: light pixels' 1000-sample chains were the
+     // launch's longest items at N = 8 (per-sample overhead, not traversal steps, sets their latency)
+    const double lanes = (double)d->chain_grid * b1::kBlock;
+    m.kmin = cfg.chain_fill > 0.0f ? (int)ceil(lanes * cfg.chain_fill / (double)npix) : 1;
+    if (m.kmin < 1) m.kmin = 1;
+  }
   m.kmax_wave = d->b1_lds_bytes ? cfg.chain_kmax_wave : 0;  // no whole waves without the LDS scene
   m.spp = V.S.cam.spp;
   m.min_seg = cfg.chain_min_seg;
