@@ -45,7 +45,7 @@ void rt_scene_release(rt_device_scene *dscene);
 /* Render rows row0, row0 + row_stride, ... (n_rows of them) into d_out (device pointer,
  * n_rows * width * 3 bytes, compact, in that row order).  Asynchronous on `stream`
  * (hipStream_t, NULL = default stream of the scene's device): no host synchronisation.  This is
- * the hot path.  Book-1 scenes at >= 32 spp first run a low-spp cost pass (RT_LPT_SPP, default 8)
+ * the hot path.  Book-1 scenes at >= 64 spp first run a low-spp cost pass (RT_LPT_SPP, default 16)
  * that plans the launch (longest-first order; split pixel streams, rt_book1.h: ChainPx); the image
  * does not depend on the plan.  Launches on one scene share its scratch, so each launch first waits
  * (on the device, hipStreamWaitEvent) for the scene's previous launch, on whatever stream that was;

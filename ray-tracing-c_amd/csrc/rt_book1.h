@@ -229,37 +229,14 @@ RT_D void sphere_test_lane(const float4 *sph, uint32_t ref, Lane &L, float tmin)
   L.hit = idx;
 }
 
-// ---------------------------------------------------------------- exact fast arithmetic
-// What sqrtf() and '/' compile to for f32 on gfx950 (denormals on, correctly rounded): a hardware
-// estimate plus a Newton / one-ulp correction core, wrapped in operand scaling for extreme exponents
-// and a special-value fix-up (v_div_scale / v_div_fmas / v_div_fixup, and the 2^-96 rescale + class
-// test of the sqrt).  On the operand ranges below the wrappers are identities, so the bare cores
-// return the same bits; the division's reciprocal refinement depends on the divisor only and is
-// hoisted per ray.  Bitwise equality is checked on the device by rt_diag_arith (all floats for the
-// sqrt, random pairs for the division: tests/test_libm_port.py).
-constexpr float kDivLo = 0x1p-20f, kDivHi = 0x1p20f;  // divisor range (|d|^2 of a ray)
-constexpr float kNumHi = 0x1p40f;                     // numerator magnitude bound
-constexpr float kSqrtLo = 0x1p-96f;                   // below it the compiler rescales
-
-RT_D float sqrt_core(float x) {  // == sqrtf(x) for x == 0 or kSqrtLo <= x < inf
-  const float r = __builtin_amdgcn_sqrtf(x);
-  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
-  float out = fmaf(-rm, r, x) <= 0.0f ? rm : r;
-  out = fmaf(-rp, r, x) > 0.0f ? rp : out;
-  return out;
-}
-RT_D float recip_core(float a) {  // the divisor half of the '/' sequence
-  const float y = __builtin_amdgcn_rcpf(a);
-  return fmaf(fmaf(-a, y, 1.0f), y, y);
-}
-RT_D float div_core(float x, float a, float ra) {  // == x / a for a in [kDivLo, kDivHi], |x| <= kNumHi
-  const float q0 = x * ra;
-  const float q1 = fmaf(fmaf(-a, q0, x), ra, q0);
-  return fmaf(fmaf(-a, q1, x), ra, q1);
-}
-// For |x| < 2^-40 (zero and denormals included) div_core is not bit-exact, but both it and x / a
-// are below 2^-18 < t_min in magnitude, so the Sphere_hit root test rejects both: the decision and
-// the recorded root (none) are the same.  Only |x| > kNumHi needs the real division.
+// exact fast arithmetic: sqrt_core / recip_core / div_core and their ranges live in rt_device.h
+using rt::div_core;
+using rt::kDivHi;
+using rt::kDivLo;
+using rt::kNumHi;
+using rt::kSqrtLo;
+using rt::recip_core;
+using rt::sqrt_core;
 
 // Sphere_hit (src/hittable.c:125-150) with the exact cores; lanes outside their ranges (NaN,
 // huge numerators, tiny discriminants, degenerate rays) evaluate the reference expression.

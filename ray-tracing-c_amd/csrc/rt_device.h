@@ -157,6 +157,38 @@ inline DScene make_view(const rt_flat_scene &s, const void *const arrays[13]) {
   return v;
 }
 
+// ------------------------------------------------------------------------------ exact fast arithmetic
+// What sqrtf() and '/' compile to for f32 on gfx950 (denormals on, correctly rounded): a hardware
+// estimate plus a Newton / one-ulp correction core, wrapped in operand scaling for extreme exponents
+// and a special-value fix-up (v_div_scale / v_div_fmas / v_div_fixup, and the 2^-96 rescale + class
+// test of the sqrt).  On the operand ranges below the wrappers are identities, so the bare cores
+// return the same bits; the division's reciprocal refinement depends on the divisor only and is
+// hoisted per ray.  Bitwise equality is checked on the device by rt_diag_arith (all floats for the
+// sqrt, random pairs for the division: tests/test_libm_port.py).
+constexpr float kDivLo = 0x1p-20f, kDivHi = 0x1p20f;  // divisor range (|d|^2 of a ray)
+constexpr float kNumHi = 0x1p40f;                     // numerator magnitude bound
+constexpr float kSqrtLo = 0x1p-96f;                   // below it the compiler rescales
+
+RT_D float sqrt_core(float x) {  // == sqrtf(x) for x == 0 or kSqrtLo <= x < inf
+  const float r = __builtin_amdgcn_sqrtf(x);
+  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
+  float out = fmaf(-rm, r, x) <= 0.0f ? rm : r;
+  out = fmaf(-rp, r, x) > 0.0f ? rp : out;
+  return out;
+}
+RT_D float recip_core(float a) {  // the divisor half of the '/' sequence
+  const float y = __builtin_amdgcn_rcpf(a);
+  return fmaf(fmaf(-a, y, 1.0f), y, y);
+}
+RT_D float div_core(float x, float a, float ra) {  // == x / a for a in [kDivLo, kDivHi], |x| <= kNumHi
+  const float q0 = x * ra;
+  const float q1 = fmaf(fmaf(-a, q0, x), ra, q0);
+  return fmaf(fmaf(-a, q1, x), ra, q1);
+}
+// For |x| < 2^-40 (zero and denormals included) div_core is not bit-exact, but both it and x / a
+// are below 2^-18 < t_min in magnitude, so the Sphere_hit root test rejects both: the decision and
+// the recorded root (none) are the same.  Only |x| > kNumHi needs the real division.
+
 // ------------------------------------------------------------------------------ primitives
 // Sphere_hit up to the accepted root (src/hittable.c:120-138); a = |d|^2 hoisted per ray.
 RT_D bool sphere_t(const rt_sphere &s, f3 o, f3 d, float a, float tmin, float tmax, float &t) {
@@ -384,6 +416,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
 struct PreTrace {
   f3 o, d, inv;            // the ray in the current frame
   float dd, tmax;
+  float ra;                // recip_core(dd): the divisor half of '/' by dd, hoisted per frame
+  bool fast;               // dd in [kDivLo, kDivHi] (div_core by dd is exact)
   int32_t frame;
   uint32_t p, fend, fpos;  // next entry; the current frame's subtree end and entry position
   bool found;
@@ -393,6 +427,8 @@ RT_D void pre_begin(PreTrace &T, f3 wo, f3 wd) {
   T.o = wo, T.d = wd;
   T.inv = mk(1.0f / wd.x, 1.0f / wd.y, 1.0f / wd.z);
   T.dd = dot(wd, wd);
+  T.ra = recip_core(T.dd);
+  T.fast = T.dd >= kDivLo && T.dd <= kDivHi;
   T.tmax = __builtin_inff();
   T.frame = RT_REF_NONE;
   T.p = 0u, T.fend = 0xffffffffu, T.fpos = 0u;

@@ -23,12 +23,173 @@ struct GeneralView {
   int32_t batch;             // kBatch: shade once this many lanes of a wave wait (RT_GEN_BATCH)
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
+  int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
+  unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
 };
+
+// -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
+enum {
+  kGsIterRefill = 0, kGsIterTrace, kGsIterShade,  // cycles of loop iterations by what they ran
+  kGsTraceIters, kGsTraceLanes, kGsShadeIters, kGsShadeLanes,
+  kGsStepKinds,                                     // sum over trace steps of distinct entry kinds present
+  kGsKindBox, kGsKindSphere, kGsKindQuad, kGsKindXform, kGsKindMedium, kGsKindOther,  // lane-steps per kind
+  kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
+  kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
+  kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsN
+};
+
+// ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
+// wave runs the rare, expensive entries -- leaving a transform's subtree, entering one (local_ray +
+// three divisions), a constant medium (two boundary roots + logf) -- only when enough of its lanes
+// wait at one (rare_min) or nothing else is left, instead of in nearly every step for one lane: at
+// scene 7, 1.5 % of lane-steps are media and 1.7 % transforms, yet ~40 % of wave-steps held one of
+// each.  A lane's own sequence of entries, t_max updates and rng draws is pre_step's, so deferral
+// changes timing only.  Boxes run branch-free and spheres on the exact cores (rt_device.h).
+
+// The ray of frame T.frame from the world ray, with its hoisted per-frame terms.
+RT_D void pre_frame_ray(const DScene &S, PreTrace &T, f3 wo, f3 wd) {
+  local_ray(S, T.frame, wo, wd, T.o, T.d);
+  T.inv = mk(1.0f / T.d.x, 1.0f / T.d.y, 1.0f / T.d.z);
+  T.dd = dot(T.d, T.d);
+  T.ra = recip_core(T.dd);
+  T.fast = T.dd >= kDivLo && T.dd <= kDivHi;
+}
+
+// true when the lane's next action is a rare one (q1: its entry, loaded by the caller)
+template <int F>
+RT_D bool pre_is_rare(const PreTrace &T, float4 q1) {
+  if ((F & RT_FEAT_XFORM) && T.p >= T.fend) return true;
+  const int kind = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, q1.w));
+  return ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) ||
+         ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM);
+}
+
+// One action of the scan (pre_step's, for the entry q0/q1 at T.p); true once past the last entry.
+// Leaving transform subtrees is an action of its own: the entry at T.p then runs in a later step.
+// pre: the preorder (S.pre, or its LDS copy when the whole of it is there: plain ds_read, no flat).
+template <int F>
+RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g, float4 q0,
+                   float4 q1) {
+  const uint32_t n = (uint32_t)S.n_pre;
+  if (T.p >= n) return true;
+  if ((F & RT_FEAT_XFORM) && T.p >= T.fend) {
+    while (T.p >= T.fend) {  // leaving a transform's subtree: the enclosing frame again
+      const uint32_t pp = __builtin_bit_cast(uint32_t, pre[2 * T.fpos].z);
+      T.frame = parent_of(S, T.frame);
+      T.fend = pp == 0xffffffffu ? 0xffffffffu : __builtin_bit_cast(uint32_t, pre[2 * pp].x);
+      T.fpos = pp == 0xffffffffu ? 0u : pp;
+    }
+    pre_frame_ray(S, T, wo, wd);
+    return false;
+  }
+  const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
+  const int kind = rt_ref_kind(ref);
+  const int32_t idx = rt_ref_index(ref);
+  const f3 o = T.o, d = T.d;
+  uint32_t next = T.p + 1;
+  float t = 0.0f;
+  bool hit = false;
+  if ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) {
+    // AABB_hit with the three slabs evaluated together (rt_book1.h: aabb_packed): t_min / t_max
+    // only tighten and fmaxf / fminf ignore NaN, so one test at the end equals the early exits
+    const float ix = T.inv.x, iy = T.inv.y, iz = T.inv.z;
+    const float ax = (q0.x - o.x) * ix, bx = (q0.w - o.x) * ix;
+    const float ay = (q0.y - o.y) * iy, by = (q1.x - o.y) * iy;
+    const float az = (q0.z - o.z) * iz, bz = (q1.y - o.z) * iz;
+    const float lo = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? bx : ax), iy < 0 ? by : ay), iz < 0 ? bz : az);
+    const float hi = fminf(fminf(fminf(T.tmax, ix < 0 ? ax : bx), iy < 0 ? ay : by), iz < 0 ? az : bz);
+    if (hi <= lo) next = __builtin_bit_cast(uint32_t, q1.z);
+  } else if (kind == RT_KIND_SPHERE) {
+    // Sphere_hit (src/hittable.c:120-138) on the exact cores, as rt_book1.h's sphere_test_data;
+    // lanes outside the cores' ranges evaluate the reference expression
+    const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
+    const float b = dot(oc, d);
+    const float c = dot(oc, oc) - q0.w;
+    const float disc = b * b - T.dd * c;
+    if (!(disc < 0)) {
+      float sq = sqrt_core(disc);
+      float r1 = div_core(-b - sq, T.dd, T.ra), r2 = div_core(-b + sq, T.dd, T.ra);
+      const bool ok = (int)T.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                      (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+      if (__builtin_expect(!ok, 0)) {
+        sq = sqrtf(disc);
+        r1 = (-b - sq) / T.dd;
+        r2 = (-b + sq) / T.dd;
+      }
+      const bool take1 = !(r1 <= tmin || r1 >= T.tmax), take2 = !(r2 <= tmin || r2 >= T.tmax);
+      hit = take1 || take2;
+      t = take1 ? r1 : r2;
+    }
+  } else if ((F & RT_FEAT_QUAD) && kind == RT_KIND_QUAD) {
+    // quad_t with the plane (normal, D) inline: the quad record is read only past the plane test
+    const f3 nq = mk(q0.x, q0.y, q0.z);
+    const float denom = dot(nq, d);
+    const float tt = (q0.w - dot(nq, o)) / denom;
+    hit = !(fabsf(denom) < 1e-8f) && !((tt < tmin) || (tt > T.tmax));
+    if (hit) {
+      const rt_quad &qd = S.quads[idx];
+      const f3 hp = sub(ray_at(o, d, tt), ld3(qd.Q));
+      const f3 w = ld3(qd.w);
+      const float alpha = dot(w, cross(hp, ld3(qd.v)));
+      const float beta = dot(w, cross(ld3(qd.u), hp));
+      hit = !((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1));
+      t = tt;
+    }
+  } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
+    T.frame = ref;
+    T.fend = __builtin_bit_cast(uint32_t, q0.x);
+    T.fpos = T.p;
+    pre_frame_ray(S, T, wo, wd);
+  } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
+    // ConstantMedium_hit (src/hittable.c:392-423), as pre_step
+    const bool inl = __builtin_bit_cast(uint32_t, q1.y) == 1u;
+    float t1, t2, nid;
+    bool both;
+    if (inl) {
+      rt_sphere sp;
+      sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
+      const float a = dot(d, d);
+      both = sphere_t(sp, o, d, a, -__builtin_inff(), __builtin_inff(), t1) &&
+             sphere_t(sp, o, d, a, t1 + 0.0001f, __builtin_inff(), t2);
+      nid = q1.x;
+    } else {
+      const rt_medium m = S.media[idx];
+      both = prim_t(S, m.boundary, o, d, -__builtin_inff(), __builtin_inff(), t1) &&
+             prim_t(S, m.boundary, o, d, t1 + 0.0001f, __builtin_inff(), t2);
+      nid = m.neg_inv_density;
+    }
+    if (both) {
+      t1 = fmaxf(t1, tmin);
+      t2 = fminf(t2, T.tmax);
+      if (!(t1 >= t2)) {
+        t1 = t1 > 0.0f ? t1 : 0.0f;
+        const float len = sqrtf(T.dd);
+        const float inside = (t2 - t1) * len;
+        const float dist = nid * rtm::logf(g.f32());
+        if (!(dist > inside)) {
+          t = t1 + dist / len;
+          hit = true;
+        }
+      }
+    }
+  }
+  if (hit) {
+    T.tmax = t;
+    T.h.t = t;
+    T.h.prim = ref;
+    T.h.xform = T.frame;
+    T.found = true;
+  }
+  T.p = next;
+  return next >= n;
+}
 
 // kBatch (scenes with a preorder, S.pre): the trace runs a few entries per wave iteration
 // (pre_step) and a wave shades only once `batch` of its lanes wait -- as rt_book1.h's v3 loop --
 // instead of every lane waiting for the wave's longest trace each bounce.
-template <int F, bool kBatch = false>
+// kAllLds: the whole preorder is in LDS (the 768/1024-thread kernels), so the scan reads only LDS.
+template <int F, bool kBatch = false, bool kAllLds = false>
 __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, float4 *lds = nullptr) {
   const DScene &S = V.S;
   const uint32_t n_lds = kBatch && lds ? (uint32_t)min(V.n_lds, S.n_pre) : 0u;
@@ -63,8 +224,31 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   PreTrace T;  // kBatch: the lane's trace in progress (tracing) or finished, not yet shaded (pending)
   T.found = false;
   bool tracing = false, pending = false;
+  uint64_t gs_c = 0;
+  (void)gs_c;
+#ifdef RT_GEN_STATS
+  unsigned long long gs[kGsN];
+  for (int q = 0; q < kGsN; q++) gs[q] = 0;
+  int gs_kind = kGsIterRefill;
+  uint64_t gs_t = __builtin_amdgcn_s_memtime();
+#define GS_NOW() __builtin_amdgcn_s_memtime()
+#define GS_ADD(k, v) (gs[k] += (unsigned long long)(v))
+#define GS_CNT(k, pred) GS_ADD(k, __popcll(__ballot(pred)))
+#else
+#define GS_NOW() 0ull
+#define GS_ADD(k, v) ((void)0)
+#define GS_CNT(k, pred) ((void)0)
+#endif
 
   for (;;) {
+#ifdef RT_GEN_STATS
+    {
+      const uint64_t now = GS_NOW();
+      gs[gs_kind] += now - gs_t;
+      gs_t = now;
+      gs_kind = kGsIterRefill;
+    }
+#endif
     // ---- refill (src/raytracing.c:93-94): lanes without a pixel take the next ones
     const uint64_t want = __ballot(need_pixel && !done);
     if (want) {
@@ -98,19 +282,61 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       const int live = (int)__popcll(tr | ready);
       const int batch = min(V.batch, (3 * live + 3) / 4);
       if (tr != 0 && (int)__popcll(ready) < batch) {  // traversal steps for the lanes still tracing
-        if (tracing) {
+#ifdef RT_GEN_STATS
+        gs_kind = kGsIterTrace;
+        GS_ADD(kGsTraceIters, 1);
+        GS_ADD(kGsTraceLanes, __popcll(tr));
+        for (int k = 0; k < V.steps; k++) {  // entry kinds the tracing lanes meet (peek, no state change)
+          const bool on = tracing && T.p < (uint32_t)S.n_pre;
+          int kind = -1;
+          if (on) {
+            const uint32_t q = T.p;
+            const float4 q1 = q < n_lds ? lds[2 * q + 1] : S.pre[2 * q + 1];
+            kind = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, q1.w));
+          }
+          const uint64_t b0 = __ballot(on && kind == RT_KIND_BVH), b1 = __ballot(on && kind == RT_KIND_SPHERE),
+                         b2 = __ballot(on && kind == RT_KIND_QUAD),
+                         b3 = __ballot(on && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)),
+                         b4 = __ballot(on && kind == RT_KIND_MEDIUM), ball = __ballot(on);
+          GS_ADD(kGsKindBox, __popcll(b0)), GS_ADD(kGsKindSphere, __popcll(b1)), GS_ADD(kGsKindQuad, __popcll(b2));
+          GS_ADD(kGsKindXform, __popcll(b3)), GS_ADD(kGsKindMedium, __popcll(b4));
+          GS_ADD(kGsKindOther, __popcll(ball & ~(b0 | b1 | b2 | b3 | b4)));
+          GS_ADD(kGsStepKinds, (b0 != 0) + (b1 != 0) + (b2 != 0) + (b3 != 0) + (b4 != 0));
+          break;  // the first step of the iteration only
+        }
+#endif
 #pragma unroll 1
-          for (int k = 0; k < V.steps; k++)
-            if (pre_step<F>(S, T, o, d, 1e-3f, g, lds, n_lds)) {
-              tracing = false;
-              pending = true;
-              break;
+        for (int k = 0; k < V.steps; k++) {
+          float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q1 = q0;
+          bool rare = false;
+          if (tracing) {
+            const uint32_t q = T.p < (uint32_t)S.n_pre ? T.p : 0u;
+            if (kAllLds || q < n_lds) {
+              q0 = lds[2 * q], q1 = lds[2 * q + 1];
+            } else {
+              q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
             }
+            rare = pre_is_rare<F>(T, q1);
+          }
+          const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
+          if ((rm | cm) == 0) break;
+          const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
+          if (tracing && (!rare || run_rare) && pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1)) {
+            tracing = false;
+            pending = true;
+          }
         }
         continue;
       }
       if (tracing) continue;  // sits out this shading pass
     }
+#ifdef RT_GEN_STATS
+    if (__ballot(!done)) {
+      gs_kind = kGsIterShade;
+      GS_ADD(kGsShadeIters, 1);
+      GS_CNT(kGsShadeLanes, !done);
+    }
+#endif
     if (done) continue;
     bool write = spp <= 0 && !need_pixel;  // no samples: the mean is 0/0 (src/raytracing.c:127)
     // ---- camera ray (src/raytracing.c:100-122)
@@ -157,27 +383,52 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         rays++;
         found = S.pre ? trace_pre<F>(S, o, d, 1e-3f, g, h) : trace<F>(S, o, d, 1e-3f, g, h);
       }
+      GS_CNT(kGsMiss, !found);
       if (!found) {
         tail = ld3(S.cam.background);
         path_done = true;
       } else {
         Rec r;
+        gs_c = GS_NOW();
         make_record<F>(S, o, d, h, r);
+        GS_ADD(kGsCycRecord, GS_NOW() - gs_c);
+        gs_c = GS_NOW();
         const f3 e = emit<F>(S, r);
+        GS_ADD(kGsCycEmit, GS_NOW() - gs_c);
         f3 dir, albedo;
         bool skip_pdf;
-        if (!scatter<F>(S, r, d, g, dir, albedo, skip_pdf)) {
+#ifdef RT_GEN_STATS
+        const rt_material &gm = S.materials[r.material];
+        GS_CNT(kGsMatLam, gm.tag == RT_MAT_LAMBERTIAN), GS_CNT(kGsMatMetal, gm.tag == RT_MAT_METAL);
+        GS_CNT(kGsMatDiel, gm.tag == RT_MAT_DIELECTRIC), GS_CNT(kGsMatIso, gm.tag == RT_MAT_ISOTROPIC);
+        GS_CNT(kGsMatEnd, gm.tag != RT_MAT_LAMBERTIAN && gm.tag != RT_MAT_METAL && gm.tag != RT_MAT_DIELECTRIC &&
+                              gm.tag != RT_MAT_ISOTROPIC);
+        const bool textured = gm.tag == RT_MAT_LAMBERTIAN || gm.tag == RT_MAT_METAL || gm.tag == RT_MAT_ISOTROPIC;
+        const int tk = textured ? S.textures[gm.texture].kind : -1;
+        GS_CNT(kGsTexSolid, tk == RT_TEX_SOLID), GS_CNT(kGsTexChecker, tk == RT_TEX_CHECKER);
+        GS_CNT(kGsTexImage, tk == RT_TEX_IMAGE), GS_CNT(kGsTexPerlin, tk == RT_TEX_PERLIN);
+        const bool gs_perlin = __ballot(tk == RT_TEX_PERLIN) != 0;
+        GS_ADD(kGsPassPerlin, gs_perlin);
+#endif
+        gs_c = GS_NOW();
+        const bool scattered = scatter<F>(S, r, d, g, dir, albedo, skip_pdf);
+#ifdef RT_GEN_STATS
+        GS_ADD(gs_perlin ? kGsCycScatterPerlin : kGsCycScatter, GS_NOW() - gs_c);
+#endif
+        if (!scattered) {
           tail = e;
           path_done = true;
         } else {
           rec_a[n] = albedo;
           if (kFull) {
             if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
+              gs_c = GS_NOW();
               if (g.f32() < prob) dir = lights_rand(S, r.p, g);
               const float sp = scatter_pdf(S, r.material, r.normal, dir);
               const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, dir);
               rec_w[n] = sp / spdf;
               weighted |= 1ull << n;
+              GS_ADD(kGsCycLights, GS_NOW() - gs_c);
             }
           }
           n++;
@@ -193,6 +444,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       }
     }
     if (!path_done && !write) continue;
+    gs_c = GS_NOW();
     if (!write) {
     // ---- fold innermost-first, accumulate, next sample / pixel (src/raytracing.c:124-131)
     f3 c = tail;
@@ -203,6 +455,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     }
     acc = add(acc, c);
     s++;
+    GS_ADD(kGsCycFold, GS_NOW() - gs_c);
     if (s < spp) {
       need_sample = true;
       continue;
@@ -220,6 +473,13 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     if (V.cost_out) V.cost_out[pix] = rays;
     need_pixel = true;
   }
+#ifdef RT_GEN_STATS
+  if (V.stats && lane == 0)
+    for (int q = 0; q < kGsN; q++) atomicAdd(V.stats + q, gs[q]);
+#endif
+#undef GS_NOW
+#undef GS_ADD
+#undef GS_CNT
 }
 
 }  // namespace gen

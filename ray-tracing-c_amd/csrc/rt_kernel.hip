@@ -134,7 +134,7 @@ template <int F, bool kBatch = false, int kThreads = gen::kBlock>
 __global__ __launch_bounds__(kThreads, kThreads == gen::kBlock ? (kBatch ? 3 : 1) : 1) void rt_general_kernel(
     gen::GeneralView V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  gen::render_general<F, kBatch>(V, out, (float4 *)lds);
+  gen::render_general<F, kBatch, kBatch && kThreads != gen::kBlock>(V, out, (float4 *)lds);
 }
 
 __global__ void rt_diag_libm_kernel(int fn, const float *x, float *out, int64_t n) {
@@ -608,7 +608,7 @@ struct Config {
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
-  int gen_batch = 56, gen_steps = 8, gen_lds = 1024;
+  int gen_batch = 56, gen_steps = 8, gen_lds = 1024, gen_rare = 8;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
@@ -679,6 +679,7 @@ struct Config {
     c.gen_big_block = env_int("RT_GEN_BIG_BLOCK", c.gen_big_block);
     c.gen_steps = env_int("RT_GEN_STEPS", 8);
     if (c.gen_steps < 1) c.gen_steps = 1;
+    c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
     return c;
   }
 };
@@ -1643,6 +1644,7 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
                            uint8_t *d_out) {
   V.batch = d->view.pre ? d->cfg.gen_batch : 0;
   V.steps = d->cfg.gen_steps;
+  V.rare_min = d->cfg.gen_rare;
   V.n_lds = d->gen_lds;
   const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
   if (V.batch && d->gen_block == 1024) {
@@ -1703,6 +1705,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     G.work_counter = d->gen_counter;
     G.order = nullptr;
     G.cost_out = nullptr;
+    G.stats = nullptr;
     const bool all = (d->features & ~kFeatBook1) != 0;
     const dim3 gg((unsigned)d->gen_grid), gb(gen::kBlock);
     if (cfg.lpt && G.S.cam.spp >= 4 * cfg.lpt_spp && npix >= 4096) {  // longest-first order (rays per pixel)
@@ -1728,9 +1731,31 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       G.order = d->lpt_order;
     }
     HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
+#ifdef RT_GEN_STATS
+    static unsigned long long *gen_stats = nullptr;  // diagnostic build only (one device)
+    if (!gen_stats) HIP_OK(hipMalloc(&gen_stats, gen::kGsN * sizeof(unsigned long long)));
+    HIP_OK(hipMemsetAsync(gen_stats, 0, gen::kGsN * sizeof(unsigned long long), st));
+    G.stats = gen_stats;
+#endif
     if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
     launch_general(d, all, gg, gb, st, G, d_out);
     HIP_OK(hipGetLastError());
+#ifdef RT_GEN_STATS
+    if (cfg.debug) {
+      unsigned long long q[gen::kGsN];
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(q, gen_stats, sizeof q, hipMemcpyDeviceToHost));
+      static const char *names[gen::kGsN] = {
+          "cyc_iter_refill", "cyc_iter_trace", "cyc_iter_shade", "trace_iters", "trace_lanes", "shade_iters",
+          "shade_lanes", "step_kinds", "kind_box", "kind_sphere", "kind_quad", "kind_xform", "kind_medium",
+          "kind_other", "cyc_record", "cyc_emit", "cyc_scatter", "cyc_lights", "cyc_fold", "mat_lam", "mat_metal",
+          "mat_diel", "mat_iso", "mat_end", "tex_solid", "tex_checker", "tex_image", "tex_perlin",
+          "cyc_scatter_perlin", "pass_perlin", "miss"};
+      fprintf(stderr, "[rtc] gen stats:");
+      for (int k = 0; k < gen::kGsN; k++) fprintf(stderr, " %s=%llu", names[k], q[k]);
+      fprintf(stderr, "\n");
+    }
+#endif
     if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
     return 0;
   }
