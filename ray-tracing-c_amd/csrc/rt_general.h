@@ -24,6 +24,7 @@ struct GeneralView {
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
   int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
+  int32_t flat;              // kBatch: common entries as one straight-line block (pre_common, RT_GEN_FLAT)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
 };
 
@@ -185,6 +186,68 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
   return next >= n;
 }
 
+// The common entries (BVH box, sphere, quad) as one straight-line block: every lane evaluates the
+// box slabs, the sphere roots and the quad plane for its entry and keeps the result of its kind, so
+// a wave whose lanes sit at all three kinds (nearly every step at scene 7) runs no kind branches;
+// only the quad's in-plane test (its record: measured no faster when loaded up front) and the
+// sphere's out-of-range fallback branch.
+// Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
+template <int F>
+RT_D bool pre_common(const DScene &S, PreTrace &T, float tmin, float4 q0, float4 q1) {
+  const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
+  const int kind = rt_ref_kind(ref);
+  const f3 o = T.o, d = T.d;
+  // box: q0 = (lo.x, lo.y, lo.z, hi.x), q1 = (hi.y, hi.z, skip, ref)
+  const float ix = T.inv.x, iy = T.inv.y, iz = T.inv.z;
+  const float ax = (q0.x - o.x) * ix, bx = (q0.w - o.x) * ix;
+  const float ay = (q0.y - o.y) * iy, by = (q1.x - o.y) * iy;
+  const float az = (q0.z - o.z) * iz, bz = (q1.y - o.z) * iz;
+  const float lo = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? bx : ax), iy < 0 ? by : ay), iz < 0 ? bz : az);
+  const float hi = fminf(fminf(fminf(T.tmax, ix < 0 ? ax : bx), iy < 0 ? ay : by), iz < 0 ? az : bz);
+  const bool skip = ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) && hi <= lo;
+  // sphere: q0 = (center, r^2)
+  const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
+  const float b = dot(oc, d);
+  const float c = dot(oc, oc) - q0.w;
+  const float disc = b * b - T.dd * c;
+  float sq = sqrt_core(disc);
+  float r1 = div_core(-b - sq, T.dd, T.ra), r2 = div_core(-b + sq, T.dd, T.ra);
+  const bool ok = (int)T.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                  (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+  if (__builtin_expect(kind == RT_KIND_SPHERE && !(disc < 0) && !ok, 0)) {
+    sq = sqrtf(disc);
+    r1 = (-b - sq) / T.dd;
+    r2 = (-b + sq) / T.dd;
+  }
+  const bool take1 = !(r1 <= tmin || r1 >= T.tmax), take2 = !(r2 <= tmin || r2 >= T.tmax);
+  bool hit = kind == RT_KIND_SPHERE && !(disc < 0) && (take1 || take2);
+  float t = take1 ? r1 : r2;
+  if (F & RT_FEAT_QUAD) {  // quad: q0 = (normal, D); the record only past the plane test
+    const f3 nq = mk(q0.x, q0.y, q0.z);
+    const float denom = dot(nq, d);
+    const float tt = (q0.w - dot(nq, o)) / denom;
+    if (kind == RT_KIND_QUAD && !(fabsf(denom) < 1e-8f) && !((tt < tmin) || (tt > T.tmax))) {
+      const rt_quad &qd = S.quads[rt_ref_index(ref)];
+      const f3 hp = sub(ray_at(o, d, tt), ld3(qd.Q));
+      const f3 w = ld3(qd.w);
+      const float alpha = dot(w, cross(hp, ld3(qd.v)));
+      const float beta = dot(w, cross(ld3(qd.u), hp));
+      hit = !((alpha < 0) || (alpha > 1) || (beta < 0) || (beta > 1));
+      t = tt;
+    }
+  }
+  if (hit) {
+    T.tmax = t;
+    T.h.t = t;
+    T.h.prim = ref;
+    T.h.xform = T.frame;
+    T.found = true;
+  }
+  const uint32_t next = skip ? __builtin_bit_cast(uint32_t, q1.z) : T.p + 1;
+  T.p = next;
+  return next >= (uint32_t)S.n_pre;
+}
+
 // kBatch (scenes with a preorder, S.pre): the trace runs a few entries per wave iteration
 // (pre_step) and a wave shades only once `batch` of its lanes wait -- as rt_book1.h's v3 loop --
 // instead of every lane waiting for the wave's longest trace each bounce.
@@ -321,7 +384,14 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
           if ((rm | cm) == 0) break;
           const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
-          if (tracing && (!rare || run_rare) && pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1)) {
+          bool fin = false;
+          if (V.flat) {
+            if (tracing && !rare) fin = pre_common<F>(S, T, 1e-3f, q0, q1);
+            else if (tracing && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+          } else if (tracing && (!rare || run_rare)) {
+            fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+          }
+          if (fin) {
             tracing = false;
             pending = true;
           }

@@ -608,7 +608,7 @@ struct Config {
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
-  int gen_batch = 56, gen_steps = 8, gen_lds = 1024, gen_rare = 8;
+  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 1;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
@@ -677,9 +677,10 @@ struct Config {
     c.gen_lds = env_int("RT_GEN_LDS", 1024);
     c.gen_big = env_flag("RT_GEN_BIG", true);
     c.gen_big_block = env_int("RT_GEN_BIG_BLOCK", c.gen_big_block);
-    c.gen_steps = env_int("RT_GEN_STEPS", 8);
+    c.gen_steps = env_int("RT_GEN_STEPS", c.gen_steps);
     if (c.gen_steps < 1) c.gen_steps = 1;
     c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
+    c.gen_flat = env_int("RT_GEN_FLAT", c.gen_flat);
     return c;
   }
 };
@@ -1645,6 +1646,7 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.batch = d->view.pre ? d->cfg.gen_batch : 0;
   V.steps = d->cfg.gen_steps;
   V.rare_min = d->cfg.gen_rare;
+  V.flat = d->cfg.gen_flat;
   V.n_lds = d->gen_lds;
   const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
   if (V.batch && d->gen_block == 1024) {
