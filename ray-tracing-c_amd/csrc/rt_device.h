@@ -407,7 +407,8 @@ RT_D bool trace(const DScene &S, f3 wo, f3 wd, float tmin, Pcg32 &g, Hit &h) {
 // again -- and skips a subtree whose box misses.  build_preorder lays that order out as entries of
 // 2 float4, so trace_pre is a scan with skips, without a stack:
 //   BVH node:   q0 = (lo.x, lo.y, lo.z, hi.x)  q1 = (hi.y, hi.z, skip, ref)  next = hit ? p+1 : skip
-//   transform:  q0 = (end, -, enclosing transform's position or ~0, -)  q1 = (-, -, end, ref)
+//   transform:  q0 = (end, a0, enclosing transform's position or ~0, a1)  q1 = (a2, -, end, ref)
+//               (translate: (a0, a1, a2) = offset; rotate_y: (a0, a1) = (cos, sin))
 //   sphere:     q0 = (center, r^2); quad: q0 = (normal, D); q1.w = ref                 next = p+1
 //   medium:     sphere boundary: q0 = its (center, r^2), q1 = (-1/density, 1 (bits), -, ref); else -
 // (skip / end = the position after the subtree; integers stored as float bits).  Lists need no
@@ -596,8 +597,14 @@ struct PreorderBuilder {
       out[2 * p + 1] = make_float4(nd.hi[1], nd.hi[2], b(size()), b((uint32_t)ref));
     } else if (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y) {
       emit(kind == RT_KIND_TRANSLATE ? s.translates[idx].child : s.rotates[idx].child, p);
-      out[2 * p] = make_float4(b(size()), 0.0f, b(enclosing), 0.0f);
-      out[2 * p + 1] = make_float4(0.0f, 0.0f, b(size()), b((uint32_t)ref));
+      // the transform itself rides in the free words: translate (q0.y, q0.w, q1.x) = offset,
+      // rotate (q0.y, q0.w) = (cos, sin), so the scan changes frames without global loads
+      const bool tr = kind == RT_KIND_TRANSLATE;
+      const float a0 = tr ? s.translates[idx].offset[0] : s.rotates[idx].cos_theta;
+      const float a1 = tr ? s.translates[idx].offset[1] : s.rotates[idx].sin_theta;
+      const float a2 = tr ? s.translates[idx].offset[2] : 0.0f;
+      out[2 * p] = make_float4(b(size()), a0, b(enclosing), a1);
+      out[2 * p + 1] = make_float4(a2, 0.0f, b(size()), b((uint32_t)ref));
     }
   }
 };
@@ -614,6 +621,18 @@ struct Rec {
   int32_t material;
   bool front;
 };
+
+// Whether a hit on material `mat` reads the record's u, v: texture_value reads them only for image
+// and checker textures (src/texture.c:12-37), and only textured materials call it.
+RT_D bool mat_uses_uv(const DScene &S, int32_t mat) {
+  const rt_material &m = S.materials[mat];
+  if (m.tag != RT_MAT_LAMBERTIAN && m.tag != RT_MAT_METAL && m.tag != RT_MAT_ISOTROPIC &&
+      m.tag != RT_MAT_DIFFUSE_LIGHT)
+    return false;
+  if (m.texture < 0) return true;  // (not built by the flattener; keep the reference's work)
+  const int k = S.textures[m.texture].kind;
+  return k == RT_TEX_IMAGE || k == RT_TEX_CHECKER;
+}
 
 // Rebuild the winner's HitRecord exactly as its hit() wrote it, then apply the enclosing
 // transforms' fix-ups innermost-first (RotateY_hit / Translate_hit post-processing).
@@ -632,8 +651,10 @@ RT_D void make_record(const DScene &S, f3 wo, f3 wd, const Hit &h, Rec &r) {
     const f3 outward = scale(sub(r.p, ld3(s.center)), s.inv_radius);
     r.front = dot(d, outward) < 0.0f;
     r.normal = r.front ? outward : neg(outward);
-    if (F & RT_FEAT_TEX_UV) {
-      r.u = (rtm::atan2f(-outward.z, outward.x) + kPi) * kInvPi * 0.5f;  // glibc-exact ports
+    // u, v (glibc-exact atan2f / acosf ports) only where the material's texture reads them (image,
+    // checker): every other texture ignores u, v, so skipping them changes no output
+    if ((F & RT_FEAT_TEX_UV) && mat_uses_uv(S, s.material)) {
+      r.u = (rtm::atan2f(-outward.z, outward.x) + kPi) * kInvPi * 0.5f;
       r.v = rtm::acosf(-outward.y) * kInvPi;
     }
     r.material = s.material;

@@ -37,7 +37,7 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsN
 };
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
@@ -48,13 +48,35 @@ enum {
 // each.  A lane's own sequence of entries, t_max updates and rng draws is pre_step's, so deferral
 // changes timing only.  Boxes run branch-free and spheres on the exact cores (rt_device.h).
 
-// The ray of frame T.frame from the world ray, with its hoisted per-frame terms.
-RT_D void pre_frame_ray(const DScene &S, PreTrace &T, f3 wo, f3 wd) {
-  local_ray(S, T.frame, wo, wd, T.o, T.d);
+// The hoisted per-frame terms of T.d.
+RT_D void pre_frame_terms(PreTrace &T) {
   T.inv = mk(1.0f / T.d.x, 1.0f / T.d.y, 1.0f / T.d.z);
   T.dd = dot(T.d, T.d);
   T.ra = recip_core(T.dd);
   T.fast = T.dd >= kDivLo && T.dd <= kDivHi;
+}
+// Apply the transform of preorder entry `pos` to (o, d): one step of local_ray's chain (translate:
+// o - offset; rotate_y: rot_y of o and d), from the entry's inline words.
+RT_D void pre_apply_xform(const float4 *pre, uint32_t pos, f3 &o, f3 &d) {
+  const float4 q0 = pre[2 * pos], q1 = pre[2 * pos + 1];
+  if (rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, q1.w)) == RT_KIND_TRANSLATE) {
+    o = sub(o, mk(q0.y, q0.w, q1.x));
+  } else {
+    o = rot_y(o, q0.y, q0.w);
+    d = rot_y(d, q0.y, q0.w);
+  }
+}
+// The ray in the frame whose transform entry is at `pos` (~0: the world), from the world ray:
+// local_ray's chain outermost first, walking the entries' enclosing positions (depth <= 8).
+RT_D void pre_chain_ray(const float4 *pre, uint32_t pos, f3 wo, f3 wd, f3 &o, f3 &d) {
+  int depth = 0;
+  for (uint32_t q = pos; q != 0xffffffffu && depth < 8; q = __builtin_bit_cast(uint32_t, pre[2 * q].z)) depth++;
+  o = wo, d = wd;
+  for (int lvl = depth - 1; lvl >= 0; lvl--) {
+    uint32_t q = pos;
+    for (int k = 0; k < lvl; k++) q = __builtin_bit_cast(uint32_t, pre[2 * q].z);
+    pre_apply_xform(pre, q, o, d);
+  }
 }
 
 // true when the lane's next action is a rare one (q1: its entry, loaded by the caller)
@@ -75,13 +97,16 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
   const uint32_t n = (uint32_t)S.n_pre;
   if (T.p >= n) return true;
   if ((F & RT_FEAT_XFORM) && T.p >= T.fend) {
-    while (T.p >= T.fend) {  // leaving a transform's subtree: the enclosing frame again
-      const uint32_t pp = __builtin_bit_cast(uint32_t, pre[2 * T.fpos].z);
-      T.frame = parent_of(S, T.frame);
-      T.fend = pp == 0xffffffffu ? 0xffffffffu : __builtin_bit_cast(uint32_t, pre[2 * pp].x);
-      T.fpos = pp == 0xffffffffu ? 0u : pp;
-    }
-    pre_frame_ray(S, T, wo, wd);
+    uint32_t pp;
+    do {  // leaving a transform's subtree: the enclosing frame again (its ref sits in its entry)
+      pp = __builtin_bit_cast(uint32_t, pre[2 * T.fpos].z);
+      const bool top = pp == 0xffffffffu;
+      T.frame = top ? RT_REF_NONE : (int32_t)__builtin_bit_cast(uint32_t, pre[2 * pp + 1].w);
+      T.fend = top ? 0xffffffffu : __builtin_bit_cast(uint32_t, pre[2 * pp].x);
+      T.fpos = top ? 0u : pp;
+    } while (T.p >= T.fend);
+    pre_chain_ray(pre, pp, wo, wd, T.o, T.d);
+    pre_frame_terms(T);
     return false;
   }
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
@@ -138,10 +163,18 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
       t = tt;
     }
   } else if ((F & RT_FEAT_XFORM) && (kind == RT_KIND_TRANSLATE || kind == RT_KIND_ROTATE_Y)) {
+    // entering: the current frame is this transform's enclosing one, so applying this transform
+    // to the current ray is local_ray's chain one step further (same operations, same order)
     T.frame = ref;
     T.fend = __builtin_bit_cast(uint32_t, q0.x);
     T.fpos = T.p;
-    pre_frame_ray(S, T, wo, wd);
+    if (kind == RT_KIND_TRANSLATE) {
+      T.o = sub(T.o, mk(q0.y, q0.w, q1.x));  // d and its terms unchanged
+    } else {
+      T.o = rot_y(T.o, q0.y, q0.w);
+      T.d = rot_y(T.d, q0.y, q0.w);
+      pre_frame_terms(T);
+    }
   } else if ((F & RT_FEAT_MEDIUM) && kind == RT_KIND_MEDIUM) {
     // ConstantMedium_hit (src/hittable.c:392-423), as pre_step
     const bool inl = __builtin_bit_cast(uint32_t, q1.y) == 1u;
@@ -405,11 +438,13 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       gs_kind = kGsIterShade;
       GS_ADD(kGsShadeIters, 1);
       GS_CNT(kGsShadeLanes, !done);
+      GS_ADD(kGsCycTop, GS_NOW() - gs_t);
     }
 #endif
     if (done) continue;
     bool write = spp <= 0 && !need_pixel;  // no samples: the mean is 0/0 (src/raytracing.c:127)
     // ---- camera ray (src/raytracing.c:100-122)
+    gs_c = GS_NOW();
     if (need_sample && !write) {
       const float px = g.between(-0.5f, 0.5f);
       const float py = g.between(-0.5f, 0.5f);
@@ -429,6 +464,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       weighted = 0;
       need_sample = false;
     }
+    GS_ADD(kGsCycCamera, GS_NOW() - gs_c);
     // ---- one bounce of path_color (rt_device.h; src/raytracing.c:39-75)
     bool path_done = false;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
@@ -441,7 +477,9 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       bool found;
       if (kBatch) {
         if (!pending) {  // start this bounce's trace; it is shaded in a later pass
+          gs_c = GS_NOW();
           pre_begin(T, o, d);
+          GS_ADD(kGsCycBegin, GS_NOW() - gs_c);
           tracing = true;
           rays++;
           continue;

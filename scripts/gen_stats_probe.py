@@ -40,7 +40,9 @@ pc = lambda v: f"{100.0 * v / max(cyc, 1):.1f}%"
 print(f"cycles: trace iters {pc(q['cyc_iter_trace'])} shade iters {pc(q['cyc_iter_shade'])} "
       f"refill-only {pc(q['cyc_iter_refill'])}")
 print(f"  in shade: record {pc(q['cyc_record'])} emit {pc(q['cyc_emit'])} scatter {pc(q['cyc_scatter'])} "
-      f"scatter(perlin passes) {pc(q['cyc_scatter_perlin'])} lights {pc(q['cyc_lights'])} fold {pc(q['cyc_fold'])}")
+      f"scatter(perlin passes) {pc(q['cyc_scatter_perlin'])} lights {pc(q['cyc_lights'])} fold {pc(q['cyc_fold'])} "
+      f"camera {pc(q.get('cyc_camera', 0))} first-bounce begin {pc(q.get('cyc_begin', 0))} "
+      f"loop top (shade iters) {pc(q.get('cyc_top', 0))}")
 ti, si = max(q["trace_iters"], 1), max(q["shade_iters"], 1)
 print(f"trace iters {q['trace_iters']} lanes/iter {q['trace_lanes'] / ti:.1f} cyc/iter {q['cyc_iter_trace'] / ti:.0f}; "
       f"shade iters {q['shade_iters']} lanes/iter {q['shade_lanes'] / si:.1f} cyc/iter {q['cyc_iter_shade'] / si:.0f}")
