@@ -37,7 +37,7 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsN
 };
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
@@ -77,6 +77,26 @@ RT_D void pre_chain_ray(const float4 *pre, uint32_t pos, f3 wo, f3 wd, f3 &o, f3
     for (int k = 0; k < lvl; k++) q = __builtin_bit_cast(uint32_t, pre[2 * q].z);
     pre_apply_xform(pre, q, o, d);
   }
+}
+
+// Sphere_hit's two candidate roots (-b -/+ sqrt(disc)) / a for the sphere q = (centre, r^2) on the
+// exact cores (a = T.dd, its reciprocal hoisted per frame), the reference expression for lanes
+// outside the cores' ranges; false when disc < 0 (no root).
+RT_D bool sphere_roots(float4 q, f3 o, f3 d, const PreTrace &T, float &r1, float &r2) {
+  const f3 oc = sub(o, mk(q.x, q.y, q.z));
+  const float b = dot(oc, d);
+  const float c = dot(oc, oc) - q.w;
+  const float disc = b * b - T.dd * c;
+  float sq = sqrt_core(disc);
+  r1 = div_core(-b - sq, T.dd, T.ra), r2 = div_core(-b + sq, T.dd, T.ra);
+  const bool ok = (int)T.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                  (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+  if (__builtin_expect(!(disc < 0) && !ok, 0)) {
+    sq = sqrtf(disc);
+    r1 = (-b - sq) / T.dd;
+    r2 = (-b + sq) / T.dd;
+  }
+  return !(disc < 0);
 }
 
 // true when the lane's next action is a rare one (q1: its entry, loaded by the caller)
@@ -181,11 +201,17 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
     float t1, t2, nid;
     bool both;
     if (inl) {
-      rt_sphere sp;
-      sp.center[0] = q0.x, sp.center[1] = q0.y, sp.center[2] = q0.z, sp.radius_sq = q0.w;
-      const float a = dot(d, d);
-      both = sphere_t(sp, o, d, a, -__builtin_inff(), __builtin_inff(), t1) &&
-             sphere_t(sp, o, d, a, t1 + 0.0001f, __builtin_inff(), t2);
+      // the two Sphere_hit calls solve the same quadratic (same o, d, centre): its roots once, on
+      // the exact cores (a = |d|^2 = T.dd), then each call's acceptance test on them
+      float r1, r2;
+      const bool real = sphere_roots(q0, o, d, T, r1, r2);
+      const float ninf = -__builtin_inff(), pinf = __builtin_inff();
+      const bool a1 = !(r1 <= ninf || r1 >= pinf), a2 = !(r2 <= ninf || r2 >= pinf);
+      t1 = a1 ? r1 : r2;
+      const float lo2 = t1 + 0.0001f;
+      const bool b1 = !(r1 <= lo2 || r1 >= pinf), b2 = !(r2 <= lo2 || r2 >= pinf);
+      t2 = b1 ? r1 : r2;
+      both = real && (a1 || a2) && (b1 || b2);
       nid = q1.x;
     } else {
       const rt_medium m = S.media[idx];
@@ -403,6 +429,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
 #endif
 #pragma unroll 1
         for (int k = 0; k < V.steps; k++) {
+          gs_c = GS_NOW();
           float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q1 = q0;
           bool rare = false;
           if (tracing) {
@@ -419,8 +446,14 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
           bool fin = false;
           if (V.flat) {
+            GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
+            gs_c = GS_NOW();
             if (tracing && !rare) fin = pre_common<F>(S, T, 1e-3f, q0, q1);
-            else if (tracing && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+            GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
+            gs_c = GS_NOW();
+            if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+            GS_ADD(kGsCycRare, GS_NOW() - gs_c);
+            GS_ADD(kGsRareSteps, run_rare);
           } else if (tracing && (!rare || run_rare)) {
             fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
           }
