@@ -169,16 +169,26 @@ constexpr float kDivLo = 0x1p-20f, kDivHi = 0x1p20f;  // divisor range (|d|^2 of
 constexpr float kNumHi = 0x1p40f;                     // numerator magnitude bound
 constexpr float kSqrtLo = 0x1p-96f;                   // below it the compiler rescales
 
+// (Host passes -- host-side checkers that include this header -- use the libm operations, which
+// the cores equal on their domains.)
 RT_D float sqrt_core(float x) {  // == sqrtf(x) for x == 0 or kSqrtLo <= x < inf
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return sqrtf(x);
+#else
   const float r = __builtin_amdgcn_sqrtf(x);
   const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
   float out = fmaf(-rm, r, x) <= 0.0f ? rm : r;
   out = fmaf(-rp, r, x) > 0.0f ? rp : out;
   return out;
+#endif
 }
 RT_D float recip_core(float a) {  // the divisor half of the '/' sequence
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return 1.0f / a;
+#else
   const float y = __builtin_amdgcn_rcpf(a);
   return fmaf(fmaf(-a, y, 1.0f), y, y);
+#endif
 }
 RT_D float div_core(float x, float a, float ra) {  // == x / a for a in [kDivLo, kDivHi], |x| <= kNumHi
   const float q0 = x * ra;

@@ -44,6 +44,9 @@ print(f"  in shade: record {pc(q['cyc_record'])} emit {pc(q['cyc_emit'])} scatte
       f"camera {pc(q.get('cyc_camera', 0))} first-bounce begin {pc(q.get('cyc_begin', 0))} "
       f"loop top (shade iters) {pc(q.get('cyc_top', 0))}")
 ti, si = max(q["trace_iters"], 1), max(q["shade_iters"], 1)
+if "cyc_common" in q:
+    print(f"  in trace: classify {pc(q['cyc_classify'])} common {pc(q['cyc_common'])} rare {pc(q['cyc_rare'])}; "
+          f"steps running rare actions {q['rare_steps']} ({100.0 * q['rare_steps'] / max(q['trace_iters'], 1):.2f} per iteration)")
 print(f"trace iters {q['trace_iters']} lanes/iter {q['trace_lanes'] / ti:.1f} cyc/iter {q['cyc_iter_trace'] / ti:.0f}; "
       f"shade iters {q['shade_iters']} lanes/iter {q['shade_lanes'] / si:.1f} cyc/iter {q['cyc_iter_shade'] / si:.0f}")
 ks = ["kind_box", "kind_sphere", "kind_quad", "kind_xform", "kind_medium", "kind_other"]
