@@ -24,7 +24,8 @@ struct GeneralView {
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
   int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
-  int32_t flat;              // kBatch: common entries as one straight-line block (pre_common, RT_GEN_FLAT)
+  int32_t flat;              // kBatch: common entries as one straight-line block (pre_common) plus up to
+                             // flat - 1 box entries in the same step (RT_GEN_FLAT; 0: branched dispatch)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
 };
 
@@ -252,7 +253,8 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
 // sphere's out-of-range fallback branch.
 // Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
 template <int F>
-RT_D bool pre_common(const DScene &S, PreTrace &T, float tmin, float4 q0, float4 q1) {
+RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin, float4 q0, float4 q1,
+                     int extra = 0) {
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
   const int kind = rt_ref_kind(ref);
   const f3 o = T.o, d = T.d;
@@ -302,7 +304,33 @@ RT_D bool pre_common(const DScene &S, PreTrace &T, float tmin, float4 q0, float4
     T.h.xform = T.frame;
     T.found = true;
   }
-  const uint32_t next = skip ? __builtin_bit_cast(uint32_t, q1.z) : T.p + 1;
+  uint32_t next = skip ? __builtin_bit_cast(uint32_t, q1.z) : T.p + 1;
+  // up to `extra` further actions in the same step while the next entry is a box (two thirds of the
+  // scan): their LDS reads and slab tests overlap the sphere / quad chains above (T.tmax as those
+  // left it); any other entry, or leaving a frame, waits for the next step
+  // (the first one straight-line, the rest in a loop: the loop's overhead measured costly at one)
+  bool more = extra > 0 && next < (uint32_t)S.n_pre && next < T.fend;
+  if (more) {
+    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
+    const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
+    const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
+    const float lo2 = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? dx : cx), iy < 0 ? dy : cy), iz < 0 ? dz : cz);
+    const float hi2 = fminf(fminf(fminf(T.tmax, ix < 0 ? cx : dx), iy < 0 ? cy : dy), iz < 0 ? cz : dz);
+    more = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) == RT_KIND_BVH;
+    if (more) next = hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1;
+  }
+#pragma unroll 1
+  for (int e = 1; more && e < extra && next < (uint32_t)S.n_pre && next < T.fend; e++) {
+    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
+    const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
+    const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
+    const float lo2 = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? dx : cx), iy < 0 ? dy : cy), iz < 0 ? dz : cz);
+    const float hi2 = fminf(fminf(fminf(T.tmax, ix < 0 ? cx : dx), iy < 0 ? cy : dy), iz < 0 ? cz : dz);
+    if (rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) != RT_KIND_BVH) break;
+    next = hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1;
+  }
   T.p = next;
   return next >= (uint32_t)S.n_pre;
 }
@@ -448,7 +476,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           if (V.flat) {
             GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, T, 1e-3f, q0, q1);
+            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
             GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
             gs_c = GS_NOW();
             if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);

@@ -608,7 +608,7 @@ struct Config {
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
-  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 1;
+  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
