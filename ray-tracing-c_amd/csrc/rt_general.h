@@ -38,7 +38,7 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsN
 };
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
@@ -527,6 +527,9 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     }
     GS_ADD(kGsCycCamera, GS_NOW() - gs_c);
     // ---- one bounce of path_color (rt_device.h; src/raytracing.c:39-75)
+#ifdef RT_GEN_STATS
+    const uint64_t gs_b = GS_NOW();
+#endif
     bool path_done = false;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     if (write) {
@@ -612,6 +615,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         }
       }
     }
+    GS_ADD(kGsCycBounce, GS_NOW() - gs_b);
     if (!path_done && !write) continue;
     gs_c = GS_NOW();
     if (!write) {
@@ -630,6 +634,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       continue;
     }
     }
+    gs_c = GS_NOW();
     const float spp_f = (float)spp;
     const float ch[3] = {acc.x, acc.y, acc.z};
     uint8_t *dst = out + pix * 3;
@@ -641,6 +646,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     }
     if (V.cost_out) V.cost_out[pix] = rays;
     need_pixel = true;
+    GS_ADD(kGsCycWrite, GS_NOW() - gs_c);
   }
 #ifdef RT_GEN_STATS
   if (V.stats && lane == 0)

@@ -1753,7 +1753,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
           "kind_other", "cyc_record", "cyc_emit", "cyc_scatter", "cyc_lights", "cyc_fold", "mat_lam", "mat_metal",
           "mat_diel", "mat_iso", "mat_end", "tex_solid", "tex_checker", "tex_image", "tex_perlin",
           "cyc_scatter_perlin", "pass_perlin", "miss", "cyc_camera", "cyc_begin", "cyc_top", "cyc_classify",
-          "cyc_common", "cyc_rare", "rare_steps"};
+          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write"};
       fprintf(stderr, "[rtc] gen stats:");
       for (int k = 0; k < gen::kGsN; k++) fprintf(stderr, " %s=%llu", names[k], q[k]);
       fprintf(stderr, "\n");

@@ -42,7 +42,8 @@ print(f"cycles: trace iters {pc(q['cyc_iter_trace'])} shade iters {pc(q['cyc_ite
 print(f"  in shade: record {pc(q['cyc_record'])} emit {pc(q['cyc_emit'])} scatter {pc(q['cyc_scatter'])} "
       f"scatter(perlin passes) {pc(q['cyc_scatter_perlin'])} lights {pc(q['cyc_lights'])} fold {pc(q['cyc_fold'])} "
       f"camera {pc(q.get('cyc_camera', 0))} first-bounce begin {pc(q.get('cyc_begin', 0))} "
-      f"loop top (shade iters) {pc(q.get('cyc_top', 0))}")
+      f"loop top (shade iters) {pc(q.get('cyc_top', 0))} whole bounce {pc(q.get('cyc_bounce', 0))} "
+      f"pixel write {pc(q.get('cyc_write', 0))}")
 ti, si = max(q["trace_iters"], 1), max(q["shade_iters"], 1)
 if "cyc_common" in q:
     print(f"  in trace: classify {pc(q['cyc_classify'])} common {pc(q['cyc_common'])} rare {pc(q['cyc_rare'])}; "
