@@ -320,8 +320,19 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     more = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) == RT_KIND_BVH;
     if (more) next = hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1;
   }
+  // the second extra action straight-line as well (extra == 2, the default), further ones looped
+  if (more && extra >= 2 && next < (uint32_t)S.n_pre && next < T.fend) {
+    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
+    const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
+    const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
+    const float lo2 = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? dx : cx), iy < 0 ? dy : cy), iz < 0 ? dz : cz);
+    const float hi2 = fminf(fminf(fminf(T.tmax, ix < 0 ? cx : dx), iy < 0 ? cy : dy), iz < 0 ? cz : dz);
+    more = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) == RT_KIND_BVH;
+    if (more) next = hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1;
+  }
 #pragma unroll 1
-  for (int e = 1; more && e < extra && next < (uint32_t)S.n_pre && next < T.fend; e++) {
+  for (int e = 2; more && e < extra && next < (uint32_t)S.n_pre && next < T.fend; e++) {
     const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
     const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
     const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
