@@ -135,6 +135,33 @@ def test_gpu_interleaved_rows_on_one_device(manifest):
     ds.close()
 
 
+@pytest.mark.parametrize("scene,width,spp", [(1, 300, 128), (5, 200, 64), (1, 300, 16)])
+def test_gpu_launches_on_two_streams_serialise(scene, width, spp):
+    """Launches on one scene share its scratch (rt_hip.h): two row bands queued back to back on two
+    streams, with no host synchronisation between them, must give the rows of a one-stream render
+    (chain render, general path and lane kernel)."""
+    import torch
+
+    sc = rtc.Scene.preset(scene, width, spp, 50)
+    ds = rtc.DeviceScene(sc, 0)
+    full = torch.empty((sc.height, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+    ds.render_rows_async(0, 1, sc.height, full.data_ptr(), torch.cuda.current_stream(0).cuda_stream)
+    torch.cuda.synchronize()
+    ref = full.cpu().numpy()
+    s1, s2 = torch.cuda.Stream(0), torch.cuda.Stream(0)
+    half = sc.height // 2
+    a = torch.empty((half, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+    b = torch.empty((sc.height - half, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    for _ in range(2):
+        ds.render_rows_async(0, 1, half, a.data_ptr(), s1.cuda_stream)
+        ds.render_rows_async(half, 1, sc.height - half, b.data_ptr(), s2.cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    _check(a.cpu().numpy(), ref[:half], f"scene {scene} band 0 on stream 1")
+    _check(b.cpu().numpy(), ref[half:], f"scene {scene} band 1 on stream 2")
+
+
 def test_gpu_rejects_out_of_range_rows():
     sc = rtc.Scene.preset(0, 40, 1, 1)
     ds = rtc.DeviceScene(sc, 0)
