@@ -280,3 +280,25 @@ def test_general_path_variants(manifest, name, env, monkeypatch):
     e = manifest["renders"][name]
     img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), f"{name} {env}")
+
+
+def test_bench_two_rank_launch_reassembles_reference_frame():
+    """bench.py's N-rank path (torch.distributed.run, rows j % N, gather, parity) run as 2 ranks on
+    this box's GPU(s) (RT_BENCH_SHARE_DEVICE=1: gloo for the reduction and the gather), on the
+    north-star scene at 10 spp: the gathered frame must be the reference render (golden
+    s1_1200x675_10spp_d50)."""
+    import json
+    import sys
+    env = dict(os.environ, RT_BENCH_SHARE_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--spp", "10", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["partition"] == "rows j % 2"
+    assert line["parity"]["golden"] == "s1_1200x675_10spp_d50"
+    assert line["parity"]["pixel_identical_to_reference"] is True
+    assert line["parity"]["max_abs_pixel_diff"] == 0
