@@ -913,8 +913,9 @@ __device__ void render_wave_items(const Book1View &V, uint8_t *__restrict__ out,
 
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
 // traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
-// 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 339 ms; frames identical -- the schedule never changes a lane)
-constexpr int kSteps = 8;
+// 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
+// schedule never changes a lane)
+constexpr int kSteps = 16;
 
 // The lane kernel.  kMode: 0 frame (whole pixels), 1 cost pre-pass (also counts draws per item),
 // 2 chain render (items of ch_items, or the continuation items of ch_cont).
