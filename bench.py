@@ -39,8 +39,9 @@ PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFM
 # the realistic ceiling for this code: non-FMA, non-packed VALU issue -- 256 CUs x 4 SIMDs
 # x 32 lanes per cycle (a wave64 VALU op issues over 2 cycles, MI355X_MICROARCH.md) x 2.4 GHz
 ISSUE_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
-PMC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_chain.json")
-PMC_CONFIG = "s1_1200x675_1000spp_d50_n1"  # the configuration the committed PMC passes profiled
+# committed rocprofv3 PMC summaries, one per configuration (scripts/gpu_profile.sh -> scripts/pmc_summary.py):
+# profiles/<round>/pmc_<config key>.json, stamped with the build id of the library they measured
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")
 
 
 def parse():
@@ -122,17 +123,22 @@ def golden_for(args):
     return None, None
 
 
-def pmc_for(kernel_name):
-    """The committed rocprofv3 PMC summary of this kernel (scripts/gpu_pmc.sh -> scripts/pmc_summary.py,
-    profiles/r02/pmc_chain.json) for the headline configuration: per-frame HBM bytes and VALU figures."""
+def pmc_for(config_key, kernel_name, build_id):
+    """The committed rocprofv3 PMC summary of this kernel at this configuration (per-frame HBM bytes and
+    VALU figures), as (path, entry, status): status "ok" only when the summary was taken with this
+    very library (same rt_build_id); "stale" when it measured another build; "none" when absent."""
+    path = os.path.join(PMC_DIR, f"pmc_{config_key}.json")
     try:
-        t = json.load(open(PMC_JSON))
+        t = json.load(open(path))
     except (OSError, ValueError):
-        return None
+        return None, None, "none"
+    rel = os.path.relpath(path, ROOT)
+    if t.get("build_id") != build_id:
+        return rel, None, "stale"
     for name, e in t.get("kernels", {}).items():
         if name.split("(")[0].replace("void ", "").replace(" ", "") == kernel_name.replace(" ", ""):
-            return e
-    return None
+            return rel, e, "ok"
+    return rel, None, "none"
 
 
 def main():
@@ -198,6 +204,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    ds.check()  # every work item of every timed launch finished (raises otherwise: no number for a partial frame)
     step_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / max(args.steps, 1)
     # the frame kernel alone (HIP events the library records around it on the same stream; the
     # step also holds the longest-first cost pre-pass and its sort): the last step's launch
@@ -269,7 +276,8 @@ def main():
         workload = (f"Book-1 final scene (reference CLI scene 1) {W}x{H}, {spp} spp, depth {args.depth}"
                     if args.scene == 1 else f"reference scene {args.scene} {W}x{H}, {spp} spp, depth {args.depth}")
         config_key = f"s{args.scene}_{W}x{H}_{spp}spp_d{args.depth}_n{world}"
-        pmc = pmc_for(kernel_name)
+        build_id = rtc.build_id()
+        pmc_src, pmc, pmc_status = pmc_for(config_key, kernel_name, build_id)
         headline = args.scene == 1 and (W, H, spp, args.depth) == (1200, 675, 1000, 50)
         line = {
             "metric": METRIC if headline else f"Msamples/s (pixels×spp) scene {args.scene} {W}×{H}×{spp}spp; max-abs pixel diff",
@@ -293,12 +301,13 @@ def main():
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 5) if achieved else None,
                          "issue_ceiling": ISSUE_TOPS,
                          "frac_of_issue_ceiling": round(achieved / ISSUE_TOPS, 5) if achieved else None,
-                         "traffic": (round(pmc["fetch_bytes"] + pmc["write_bytes"]) if pmc and "fetch_bytes" in pmc
-                                     and "write_bytes" in pmc and config_key == PMC_CONFIG else None),
+                         "traffic": (round(pmc["fetch_bytes"] + pmc["write_bytes"])
+                                     if pmc and "fetch_bytes" in pmc and "write_bytes" in pmc else None),
                          "pmc": ({k: round(pmc[k], 4) for k in ("valu_busy", "lanes_active", "valu_insts_per_sample",
-                                                                "lds_bank_conflict_frac") if k in pmc}
-                                 if pmc and config_key == PMC_CONFIG else None),
-                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc and config_key == PMC_CONFIG else None,
+                                                                "lds_bank_conflict_frac", "kernel_ms_per_frame")
+                                  if k in pmc} if pmc else pmc_status if pmc_status == "stale" else None),
+                         "pmc_source": pmc_src if pmc else None,
+                         "build_id": build_id,
                          "kernel": kernel_name, "kernel_ms_avg": round(kernel_ms, 3),
                          "step_ms_avg": round(step_ms, 3),
                          "kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
@@ -308,7 +317,8 @@ def main():
                                  "not apply). peak = dense f32 rate (FMA = 2); issue_ceiling = non-FMA non-packed "
                                  "VALU lane-ops/s (256 CU x 4 SIMD x 32 lanes x 2.4 GHz), the realistic ceiling for "
                                  "bit-exact code (no contraction). achieved counts algorithmic FP32 ops only; traffic "
-                                 "= FETCH_SIZE x 2 + WRITE_SIZE bytes per frame from the committed PMC pass"},
+                                 "= FETCH_SIZE x 2 + WRITE_SIZE bytes per frame from the committed PMC pass of "
+                                 "this build (build_id); pmc 'stale' = the committed pass measured another build"},
             "cpu_baseline": base,
             "end_to_end": e2e,
             "parity": parity,

@@ -53,10 +53,18 @@ void rt_scene_release(rt_device_scene *dscene);
 int rt_render_rows_async(rt_device_scene *dscene, int row0, int row_stride, int n_rows, uint8_t *d_out,
                          void *stream);
 
+/* Completion status of the launches made on dscene since the last call: waits for the scene's last
+ * launch, then returns 0 when every work item of its chain launches finished, or -1 (rt_last_error
+ * names the number of unfinished items; the frame written is then not valid).  Clears the status.
+ * rt_render_rows_async cannot report this itself (it returns before the work runs). */
+int rt_scene_check(rt_device_scene *dscene);
+
 /* Whole frame into a host buffer (width*height*3), rows interleaved j mod n_gpus over GPUs
  * 0..n_gpus-1 (n_gpus <= 0: all visible), no collectives.  The host-side preprocessing of the scene
- * runs once; then one host thread per GPU uploads, launches on its own stream and copies its rows
- * back.  Synchronous.  This is what Camera_render calls. */
+ * runs once; then one host thread per GPU uploads, launches on its own stream, copies its rows back
+ * and checks its completion status (rt_scene_check).  Synchronous; 0 only when every pixel of every
+ * share was rendered.  This is what Camera_render calls.  RT_REHEARSE_DEVICES=N: run as if N
+ * devices were visible (share g on device g % visible count). */
 int rt_render(const rt_flat_scene *scene, int n_gpus, uint8_t *out_host);
 
 /* Kernel-side timing of the last rt_render call on `device`: milliseconds between HIP events
@@ -100,6 +108,9 @@ const char *rt_scene_kernel(const rt_device_scene *dscene);
 
 const char *rt_last_error(void);
 int rt_abi_version(void);
+/* A hash of the library's sources and compile flags (16 hex digits): profiles under profiles/ record
+ * the id of the build they measured, and bench.py attaches their counters only to that build. */
+const char *rt_build_id(void);
 
 #ifdef __cplusplus
 }

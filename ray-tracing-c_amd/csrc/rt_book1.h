@@ -78,14 +78,21 @@ struct ChainCont {     // 32 B: a continuation item -- the true chain from an ex
 // samples / records so far, colour sum, coupling cursor) -- to a wave whose lanes have all finished,
 // which runs it on to the end with whole-wave traces (render_item_coop).
 // Control words at V.mig (uint32): [0] done: the launch's finished items; [1] helpers: waves that
-// have become helpers; then kMigBoxes mailboxes of one 128-B line each:
+// have become helpers; [2] fault injection (tests): items dropped so far; then kMigBoxes mailboxes of
+// one 128-B line each:
 //   push / pop: indices into the mailbox's part of the queue; credits: its idle helpers not yet
-//   claimed by a push (a lane pushes only against a credit, so a queued item always has a helper);
+//   claimed by a push (a lane pushes only against a credit, so a queued item always has a helper;
+//   a helper leaves only by taking back a credit nobody has claimed);
 //   finished: set once every item is done (the helpers' exit).
 // Helpers poll only their own mailbox's line, rarely: thousands of idle waves polling one address
 // would swamp that memory channel and slow every working lane (measured: +30 % at N = 8).
+// After the launch, chain_check_kernel compares [0] with the launch's item count: a launch that
+// finished fewer items than it was given is reported through the scene's status word.
 constexpr int kMigBoxes = 64, kMigBoxWords = 32;
-enum : int { kMigDone = 0, kMigHelpers = 1, kMigBox0 = 32, kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3 };
+enum : int {
+  kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigBox0 = 32,
+  kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3
+};
 constexpr int kMigWords = kMigBox0 + kMigBoxes * kMigBoxWords;
 constexpr int kMigMode = 2;  // the launches that migrate: chain launches (kMode 2)
 struct MigRec {       // 64 B
@@ -162,6 +169,8 @@ struct Book1View {
   int32_t mig_max_help;  // at most this many finished waves stay as helpers; the others leave.  Resident
                          // idle waves slow the working ones (measured: all 5120 waves of a grid kept
                          // resident made N = 8 shares 20 % slower, however rarely they polled)
+  uint32_t mig_drop;     // fault injection (tests only): helpers drop this many popped items unrun
+  uint64_t mig_wait;     // a helper idle this long (wall_clock64 ticks, 100 MHz) offers to leave
 };
 
 // ---------------------------------------------------------------- pixel output
@@ -842,20 +851,40 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
       MigRec r = *q;
       r.pix = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.pix);
       r.seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.seg);
-      __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
-      render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
-      __builtin_amdgcn_s_setprio(0);
-      if (l0) {
-        mig_item_done(V, total_own);
-        atomicAdd(box + kMigCredits, 1u);
+      // (fault injection, tests only: drop the item unrun and uncounted -- chain_check_kernel must
+      // then report the launch as incomplete)
+      int drop = 0;
+      if (V.mig_drop && l0) drop = atomicAdd(&V.mig[kMigDropped], 1u) < V.mig_drop;
+      if (!__builtin_amdgcn_readfirstlane(drop)) {
+        __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
+        render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
+        __builtin_amdgcn_s_setprio(0);
+        if (l0) mig_item_done(V, total_own);
       }
+      if (l0) atomicAdd(box + kMigCredits, 1u);
       idle_since = wall_clock64();
       continue;
     }
     if (__builtin_amdgcn_readfirstlane(fin)) break;
-    // (a bound on the wait, so that a protocol bug cannot hang the GPU: no launch idles a helper for
-    // seconds; the image would then be wrong, which the parity tests report)
-    if (wall_clock64() - idle_since > 400000000ull) break;  // 4 s at 100 MHz
+    // A helper idle for mig_wait leaves -- but only by taking back a credit that no push has claimed.
+    // A claimed credit stands for an item that is (being) queued in this mailbox, which then still
+    // has a helper to run it; so no item is ever queued to a mailbox whose helpers have all left.
+    // (Every item done sets kMigFinished; the bound only frees CU slots in long tails.)
+    if (wall_clock64() - idle_since > V.mig_wait) {
+      int left = 0;
+      if (l0) {
+        uint32_t c = ld_rel(box + kMigCredits);
+        while ((int32_t)c > 0) {
+          const uint32_t prev = atomicCAS(box + kMigCredits, c, c - 1u);
+          if (prev == c) {
+            left = 1;
+            break;
+          }
+          c = prev;
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane(left)) break;
+    }
     for (int k = 0; k < V.mig_sleep; k++) __builtin_amdgcn_s_sleep(127);  // ~3.4 us each
   }
 }

@@ -577,6 +577,22 @@ __global__ void chain_fill_kernel(const uint32_t *cnt, uint32_t *ch_end, uint32_
 constexpr size_t kCounterBytes = 128 + b1::kMigWords * sizeof(uint32_t);  // work counter line + migration words
 constexpr size_t kCounterSlot = (kCounterBytes + 255) / 256 * 256;
 
+// After a migrating chain launch: did every work item finish?  A lane or helper counts each item it
+// completes (rt_book1.h: mig_item_done); fewer than the launch's items means work was lost, which the
+// scene's status word records (rt_scene_check surfaces it; rt_render / Camera_render fail loudly).
+// status[0]: error bits (1: items unfinished), status[1]: items missing (summed over launches).
+enum : uint32_t { kStatusIncomplete = 1u };
+__global__ void chain_check_kernel(const uint32_t *mig, const uint32_t *n_items, const uint32_t *n_coop,
+                                   uint32_t *status) {
+  if (threadIdx.x != 0) return;
+  const uint32_t total = *n_items - (n_coop ? *n_coop : 0u);
+  const uint32_t done = mig[b1::kMigDone];
+  if (done != total) {
+    atomicOr(&status[0], kStatusIncomplete);
+    atomicAdd(&status[1], total > done ? total - done : 1u);
+  }
+}
+
 // ------------------------------------------------------------------------------ configuration
 static bool env_flag(const char *name, bool dflt) {
   const char *e = getenv(name);
@@ -615,6 +631,8 @@ struct Config {
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
+  int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
+  int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
   int lane_occ = 5;   // lane kernel occupancy target
   int sample_cost = 0;     // cost pre-pass: per-sample latency in traversal steps (measured: 75-250 slower; off)
@@ -630,6 +648,10 @@ struct Config {
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
+    c.mig_wait_us = env_int("RT_MIG_WAIT_US", c.mig_wait_us);
+    if (c.mig_wait_us < 0) c.mig_wait_us = 0;
+    c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
+    if (c.mig_drop < 0) c.mig_drop = 0;
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.book1 = env_flag("RT_BOOK1", true);
@@ -697,6 +719,7 @@ struct rt_device_scene {
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
   hipEvent_t ev_done = nullptr;                // end of the last launch: the next one waits for it
   bool launched = false;
+  uint32_t *status = nullptr;  // device: completion status of the launches (chain_check_kernel)
   // Book-1 path (rt_book1.h), when the scene qualifies
   bool book1 = false;
   b1::Book1View b1view;
@@ -1278,8 +1301,9 @@ static rt_device_scene *upload_packed(const rt_flat_scene *s, const HostPack &H,
     d->view.n_pre = (int32_t)(H.pre.size() / 2);
   }
   if (hipEventCreate(&d->ev_main[0]) != hipSuccess || hipEventCreate(&d->ev_main[1]) != hipSuccess ||
-      hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) {
-    rt_set_error("event creation failed on device %d", device);
+      hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&d->status, 256) != hipSuccess || hipMemset(d->status, 0, 256) != hipSuccess) {
+    rt_set_error("event / status word creation failed on device %d", device);
     rt_scene_release(d);
     return NULL;
   }
@@ -1328,6 +1352,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->pre_arena) (void)hipFree(d->pre_arena);
   if (d->ch_arena) (void)hipFree(d->ch_arena);
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
+  if (d->status) (void)hipFree(d->status);
   if (d->wave_stream) (void)hipStreamDestroy(d->wave_stream);
   if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
   if (d->ev_join) (void)hipEventDestroy(d->ev_join);
@@ -1488,12 +1513,17 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_idle = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_idle / 100);
   V.mig_sleep = cfg.mig_sleep;
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
+  V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
+  V.mig_drop = (uint32_t)cfg.mig_drop;
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   launch_chain_kernel(d, V, d_out, st);  // (whole-wave items in its first waves: rt_book1.h coop_items)
   HIP_OK(hipGetLastError());
+  if (V.mig_live > 0)  // (before the continuation launch resets the migration words)
+    hipLaunchKernelGGL(chain_check_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)V.mig, V.ch_n_items, V.n_coop,
+                       d->status);
   hipEvent_t dbg_ev[3] = {nullptr, nullptr, nullptr};  // (RT_DEBUG: chains / fold / continuations)
   if (cfg.debug) {
     for (auto &e : dbg_ev) HIP_OK(hipEventCreate(&e));
@@ -1525,6 +1555,9 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   launch_chain_kernel(d, C, d_out, st);
   HIP_OK(hipGetLastError());
+  if (C.mig_live > 0)
+    hipLaunchKernelGGL(chain_check_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)C.mig, C.ch_n_cont,
+                       (const uint32_t *)nullptr, d->status);
   if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
   if (cfg.debug) {
     HIP_OK(hipEventRecord(dbg_ev[2], st));
@@ -1800,6 +1833,20 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
   return rc;
 }
 
+// Completion status of the scene's launches so far (chain_check_kernel): waits for the last launch,
+// then returns 0, or -1 with the number of unfinished work items in the error message, and clears it.
+extern "C" int rt_scene_check(rt_device_scene *d) {
+  if (!d) return rt_set_error("rt_scene_check: NULL scene"), -1;
+  HIP_OK(hipSetDevice(d->device));
+  if (d->launched) HIP_OK(hipEventSynchronize(d->ev_done));
+  uint32_t st[2] = {0u, 0u};
+  HIP_OK(hipMemcpy(st, d->status, sizeof st, hipMemcpyDeviceToHost));
+  if (st[0] == 0u) return 0;
+  HIP_OK(hipMemset(d->status, 0, sizeof st));
+  return rt_set_error("render incomplete on device %d: %u work item(s) of a chain launch never finished "
+                      "(status 0x%x); the frame is not valid", d->device, st[1], st[0]), -1;
+}
+
 // ------------------------------------------------------------------------------ whole frame
 static std::mutex g_timing_mu;
 static std::vector<double> g_kernel_ms(64, 0.0);
@@ -1811,10 +1858,11 @@ extern "C" double rt_last_kernel_ms(int device) {
 
 // One device's share of rt_render: upload, launch, copy back its compact rows, scatter them into
 // rows j % G == g of the caller's buffer (disjoint rows: no lock).
-static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G, uint8_t *out_host, std::string &err) {
+static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G, int device, uint8_t *out_host,
+                        std::string &err) {
   const int H_img = s->camera.height, W = s->camera.width;
   const int n_rows = (H_img - g + G - 1) / G;
-  rt_device_scene *scene = upload_packed(s, H, g);
+  rt_device_scene *scene = upload_packed(s, H, device);
   if (!scene) {
     err = rt_last_error();
     return -1;
@@ -1839,7 +1887,9 @@ static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G,
     hipError_t e = hipStreamSynchronize(stream);
     if (e == hipSuccess) e = hipMemcpy(rows.data(), d_out, rows.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
-      rt_set_error("rt_render: device %d: %s", g, hipGetErrorString(e));
+      rt_set_error("rt_render: share %d (device %d): %s", g, device, hipGetErrorString(e));
+      rc = -1;
+    } else if (rt_scene_check(scene) != 0) {  // never a partial image with rc 0
       rc = -1;
     } else {
       float ms = 0.0f;
@@ -1853,7 +1903,7 @@ static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G,
     }
   }
   if (rc != 0) err = rt_last_error();
-  (void)hipSetDevice(g);
+  (void)hipSetDevice(device);
   if (t0) (void)hipEventDestroy(t0);
   if (t1) (void)hipEventDestroy(t1);
   if (d_out) (void)hipFree(d_out);
@@ -1862,21 +1912,30 @@ static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G,
   return rc;
 }
 
+// RT_REHEARSE_DEVICES=N (N > 0): behave as if N devices were visible -- share g runs on device
+// g % (visible devices), still one host thread and one device scene per share -- so the multi-device
+// path (threads, per-share upload, streams, error aggregation) runs on a box with fewer GPUs.
+// Shares on one device split its chain-record budget.  Timings are then contended.
 extern "C" int rt_render(const rt_flat_scene *s, int n_gpus, uint8_t *out_host) {
   if (!s || !out_host) return rt_set_error("rt_render: NULL argument"), -1;
   const int avail = rt_device_count();
   if (avail <= 0) return rt_set_error("rt_render: no HIP device visible (this library has no CPU path)"), -1;
-  int G = (n_gpus <= 0 || n_gpus > avail) ? avail : n_gpus;
+  const int rehearse = env_int("RT_REHEARSE_DEVICES", 0);
+  const int visible = rehearse > 0 ? rehearse : avail;
+  int G = (n_gpus <= 0 || n_gpus > visible) ? visible : n_gpus;
   if (G > s->camera.height) G = s->camera.height;
   HostPack H;  // host preprocessing once, shared by every device
   if (host_pack(s, H) != 0) return -1;
+  const int per_dev = (G + avail - 1) / avail;  // shares per device (> 1 only when rehearsing)
+  if (per_dev > 1) H.cfg.chain_mb /= (size_t)per_dev;
   std::vector<int> rc(G, 0);
   std::vector<std::string> err(G);
   if (G == 1) {
-    rc[0] = render_share(s, H, 0, 1, out_host, err[0]);
-  } else {  // one host thread per device: uploads and launches proceed in parallel
+    rc[0] = render_share(s, H, 0, 1, 0, out_host, err[0]);
+  } else {  // one host thread per share: uploads and launches proceed in parallel
     std::vector<std::thread> th;
-    for (int g = 0; g < G; g++) th.emplace_back([&, g] { rc[g] = render_share(s, H, g, G, out_host, err[g]); });
+    for (int g = 0; g < G; g++)
+      th.emplace_back([&, g] { rc[g] = render_share(s, H, g, G, g % avail, out_host, err[g]); });
     for (auto &t : th) t.join();
   }
   for (int g = 0; g < G; g++)
@@ -1930,10 +1989,11 @@ extern "C" int rt_scene_px_time(rt_device_scene *d, uint32_t *times, uint32_t *c
   return 0;
 }
 
-// Diagnostics of the last chain launch (RT_PX_TIME=1 at upload): one row of 8 u32 per work item, in
+// Diagnostics of the last chain launch (RT_PX_TIME=1 at upload): one row of 16 u32 per work item, in
 // item order -- pixel, segment, K, whole-wave (1) or lane (0), start, end (wall_clock64 ticks, low 32
-// bits), records (samples for segment 0 / unsplit), end flags (bit 0 linked, bit 1 ended).  Returns
-// the number of items (rows written: min(items, max_rows)), or -1.
+// bits), records (samples for segment 0 / unsplit), end flags (bit 0 linked, bit 1 ended), link
+// segment, link record, segment length, the pixel's pre-pass draws and cost, 3 reserved (rt_hip.h).
+// Returns the number of items (rows written: min(items, max_rows)), or -1.
 extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64_t max_rows) {
   if (!d || !d->book1 || !d->px_time || !d->seg_time) return rt_set_error("rt_scene_chain_diag: upload with RT_PX_TIME=1"), -1;
   HIP_OK(hipSetDevice(d->device));

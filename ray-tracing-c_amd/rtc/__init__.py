@@ -138,14 +138,22 @@ def lib() -> ctypes.CDLL:
         L.rt_scene_last_launch_ms.restype = c_double
         L.rt_scene_kernel.argtypes = [c_void_p]
         L.rt_scene_kernel.restype = c_char_p
+        L.rt_scene_check.argtypes = [c_void_p]
+        L.rt_scene_check.restype = c_int
         L.rt_last_error.restype = c_char_p
         L.rt_abi_version.restype = c_int
+        L.rt_build_id.restype = c_char_p
         _lib = L
     return _lib
 
 
 def last_error() -> str:
     return (lib().rt_last_error() or b"").decode(errors="replace")
+
+
+def build_id() -> str:
+    """Hash of the loaded library's sources and flags (rt_hip.h: rt_build_id)."""
+    return (lib().rt_build_id() or b"").decode()
 
 
 class Scene:
@@ -248,6 +256,12 @@ class DeviceScene:
                                         c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
         if rc != 0:
             raise RtcError(f"rt_render_rows_async failed: {last_error()}")
+
+    def check(self):
+        """Wait for this scene's launches and raise RtcError if any work item never finished
+        (rt_scene_check): the rows written are then not a valid frame."""
+        if lib().rt_scene_check(self._h) != 0:
+            raise RtcError(f"rt_scene_check: {last_error()}")
 
     def last_launch_ms(self) -> float:
         """Duration of the last frame launch (excludes the cost pre-pass); call after it completed."""

@@ -14,4 +14,4 @@ for i in "${!P[@]}"; do
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/${TAG}_p$i.log; exit $rc; fi
   dirs="$dirs gpurun_out/${TAG}_p$i"
 done
-python3 scripts/pmc_summary.py gpurun_out/${TAG}_summary.json ${SAMPLES:-1} $dirs
+python3 scripts/pmc_summary.py gpurun_out/${TAG}_summary.json --build-id "${BID:-unknown}" --config "${KEY:-custom}" --samples-per-frame "${SAMPLES:-1}" $dirs

@@ -1,42 +1,70 @@
-"""Per-kernel rocprofv3 counter totals from scripts/gpu_pmc.sh passes, as JSON.
+"""Per-kernel, per-frame rocprofv3 summary of one bench configuration, stamped with the build id.
 
-    python scripts/pmc_summary.py OUT.json SAMPLES DIR [DIR ...]
+    python scripts/pmc_summary.py OUT.json --build-id ID --config KEY --samples-per-frame S \
+        [--stats DIR --stats-frames F] [--pmc-frames F DIR [DIR ...]]
 
-Sums counter_collection.csv values per kernel name over all dispatches in each pass directory and
-derives, per kernel (SAMPLES = samples of the frames the passes profiled):
-  valu_insts_per_sample  SQ_INSTS_VALU / SAMPLES (wave-level instructions)
+--stats DIR: a `rocprofv3 --kernel-trace --stats` run of `bench.py` (F frames in all, warmup
+included): per kernel the calls, total ns and ms per frame (= total / F; the chain kernel is two
+dispatches per frame, the launch and its -- normally empty -- continuation, so AverageNs is not the
+per-frame time).
+--pmc-frames F DIR...: `rocprofv3 --pmc` passes (scripts/gpu_profile.sh), each over F frames.  Sums the
+counter values per kernel over all dispatches of a pass and derives, per kernel:
+  valu_insts_per_sample  SQ_INSTS_VALU / (F x S) (wave-level instructions)
   lanes_active           SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU (active lanes per VALU issue)
   valu_busy              SQ_ACTIVE_INST_VALU x 2 cycles (a wave64 VALU op issues over 2 cycles on a
-                         SIMD-32, MI355X_MICROARCH.md) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): the
-                         share of SIMD cycles issuing VALU (GRBM_GUI_ACTIVE sums the 8 XCDs' clocks)
+                         SIMD-32, MI355X_MICROARCH.md) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
   lds_bank_conflict_frac SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-  fetch_bytes / write_bytes  FETCH_SIZE x 2 / WRITE_SIZE in bytes (KB x 1024; FETCH doubled per
-                         MI355X_MICROARCH.md: gfx950 tallies 128-B read requests at 64 B)
+  fetch_bytes / write_bytes  per frame: FETCH_SIZE x 2 / WRITE_SIZE in bytes (KB x 1024; FETCH doubled
+                         per MI355X_MICROARCH.md: gfx950 tallies 128-B read requests at 64 B)
+bench.py attaches a summary to its line only when its build_id equals the timed library's.
 """
+import argparse
 import collections
 import csv
 import glob
 import json
-import sys
+
+KEEP = ("rt_book1", "rt_render", "rt_general", "chain_", "lpt_")
 
 
 def main():
-    out, samples, dirs = sys.argv[1], float(sys.argv[2]), sys.argv[3:]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--build-id", required=True)
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--samples-per-frame", type=float, required=True)
+    ap.add_argument("--stats")
+    ap.add_argument("--stats-frames", type=int, default=1)
+    ap.add_argument("--pmc-frames", type=int, default=1)
+    ap.add_argument("pmc", nargs="*")
+    a = ap.parse_args()
+    res = collections.defaultdict(dict)
+    if a.stats:
+        for f in glob.glob(f"{a.stats}/**/*kernel_stats.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                if not any(k in r["Name"] for k in KEEP):
+                    continue
+                e = res[r["Name"]]
+                e["calls"] = int(r["Calls"])
+                e["total_ns"] = float(r["TotalDurationNs"])
+                e["kernel_ms_per_frame"] = float(r["TotalDurationNs"]) / a.stats_frames / 1e6
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
-    for d in dirs:
+    for d in a.pmc:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
-                name = r["Kernel_Name"]
-                agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[name].add((d, r.get("Dispatch_Id", "")))
-    res = {}
+                agg[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    F, S = a.pmc_frames, a.samples_per_frame
     for name, c in agg.items():
-        if not any(k in name for k in ("rt_book1", "rt_render", "rt_general", "chain_")):
+        if not any(k in name for k in KEEP):
             continue
-        e = {"counters": dict(c), "dispatches_per_pass": max(1, len(disp[name]) // max(1, len(dirs)))}
+        e = res[name]
+        e["counters_per_frame"] = {k: v / F for k, v in c.items()}
         if c.get("SQ_INSTS_VALU"):
-            e["valu_insts_per_sample"] = c["SQ_INSTS_VALU"] / samples
+            e["valu_insts_per_sample"] = c["SQ_INSTS_VALU"] / (F * S)
+        if c.get("SQ_INSTS_LDS"):
+            e["lds_insts_per_sample"] = c["SQ_INSTS_LDS"] / (F * S)
+        if c.get("SQ_INSTS_VMEM_RD"):
+            e["vmem_rd_insts_per_sample"] = c["SQ_INSTS_VMEM_RD"] / (F * S)
         if c.get("SQ_ACTIVE_INST_VALU"):
             e["lanes_active"] = c.get("SQ_THREAD_CYCLES_VALU", 0.0) / c["SQ_ACTIVE_INST_VALU"]
             if c.get("GRBM_GUI_ACTIVE"):
@@ -44,13 +72,18 @@ def main():
         if c.get("SQ_LDS_IDX_ACTIVE"):
             e["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"]
         if "FETCH_SIZE" in c:
-            e["fetch_bytes"] = c["FETCH_SIZE"] * 1024 * 2
+            e["fetch_bytes"] = c["FETCH_SIZE"] * 1024 * 2 / F
         if "WRITE_SIZE" in c:
-            e["write_bytes"] = c["WRITE_SIZE"] * 1024
-        res[name] = e
-    json.dump({"samples": samples, "passes": dirs, "kernels": res}, open(out, "w"), indent=1, sort_keys=True)
+            e["write_bytes"] = c["WRITE_SIZE"] * 1024 / F
+        if "fetch_bytes" in e and "write_bytes" in e:
+            e["traffic_bytes_per_sample"] = (e["fetch_bytes"] + e["write_bytes"]) / S
+    out = {"build_id": a.build_id, "config": a.config, "samples_per_frame": S, "stats_dir": a.stats,
+           "stats_frames": a.stats_frames, "pmc_passes": a.pmc, "pmc_frames": F,
+           "note": "per-frame figures: totals / frames; bytes per frame", "kernels": res}
+    json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
     for name, e in res.items():
-        print(name, {k: (round(v, 4) if isinstance(v, float) else v) for k, v in e.items() if k != "counters"})
+        print(name[:60], {k: (round(v, 4) if isinstance(v, float) else v) for k, v in e.items()
+                          if k not in ("counters_per_frame",)})
 
 
 if __name__ == "__main__":
