@@ -66,9 +66,28 @@ struct ChainPx {       // 32 B per pixel of a chain launch (chain_plan_kernel)
   uint32_t end0;       // segment k's end word at ch_seg[end0 + k]
   uint32_t check;      // a segment >= 1 looks for the pixel's end once it holds this many records
   uint32_t cap_last;   // records of the last segment (it takes whatever remains of the stream)
-  uint32_t pad;
+  uint32_t kd;         // run-time re-cut (RecutReq): dynamic segments published (low 8 bits; atomic);
+                       // bit 8 while one is being published
 };
-RT_D uint32_t seg_cap(const ChainPx &P, uint32_t k) { return k + 1u == P.K ? P.cap_last : P.cap; }
+// Run-time re-cut.  The last segment of a pixel absorbs the whole error of the planner's stream
+// length estimate (the tail of an N-GPU share: DESIGN.md §5).  Once the launch has idle helper waves,
+// a running last segment k asks for a cut (RecutReq); a helper appends segment t = k + 1 at an offset
+// ahead of k -- the remaining true samples R (exact: spp minus what the links already cover) times the
+// chain's own draws per sample, times a fraction -- with a record list of its own, publishes it
+// (ChainPx.kd) and runs it.  Segment k then couples into t exactly like into a planned successor, and
+// t, now the last, may be cut again.  Segments stay ordered by start offset, so links still point
+// forward and the fold is unchanged.  Dynamic segment t (K <= t < K + kDynMax) has its start offset
+// and record base in ch_dyn[end0 + t]; its end word is ch_seg[end0 + t] (the planner reserves
+// K + kDynMax end words per split pixel).
+constexpr uint32_t kDynMax = 8;
+constexpr uint32_t kStUnknown = 0xffffffffu;  // coupling cursor on a dynamic successor whose start is not read yet
+struct RecutReq {      // 32 B: a last segment asking to be cut (pushed by its lane / helper wave)
+  uint32_t pix, seg;
+  uint32_t x, s;       // the chain's stream offset and records at the request
+  uint32_t wave;       // 1: the chain runs on a whole wave (fast), 0: in a lane
+  uint32_t ready;      // the launch's epoch, written last (release)
+  uint32_t pad[2];
+};
 struct ChainCont {     // 32 B: a continuation item -- the true chain from an exact position
   uint32_t pix, o, s, pad;
   float acc[4];
@@ -88,9 +107,10 @@ struct ChainCont {     // 32 B: a continuation item -- the true chain from an ex
 // would swamp that memory channel and slow every working lane (measured: +30 % at N = 8).
 // After the launch, chain_check_kernel compares [0] with the launch's item count: a launch that
 // finished fewer items than it was given is reported through the scene's status word.
+// Words [32, 64) (their own line): the re-cut request queue's push / pop indices.
 constexpr int kMigBoxes = 64, kMigBoxWords = 32;
 enum : int {
-  kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigBox0 = 32,
+  kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigRqPush = 32, kMigRqPop = 33, kMigBox0 = 64,
   kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3
 };
 constexpr int kMigWords = kMigBox0 + kMigBoxes * kMigBoxWords;
@@ -121,6 +141,7 @@ RT_D uint32_t ld_rel(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_R
 RT_D uint64_t ld_rel64(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D void st_rel(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D void st_rel64(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+RT_D uint32_t ld_acq(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
 
 struct Book1View {
   DScene S;                  // full scene (global memory): sphere aux data, camera
@@ -171,7 +192,32 @@ struct Book1View {
                          // resident made N = 8 shares 20 % slower, however rarely they polled)
   uint32_t mig_drop;     // fault injection (tests only): helpers drop this many popped items unrun
   uint64_t mig_wait;     // a helper idle this long (wall_clock64 ticks, 100 MHz) offers to leave
+  // run-time re-cut (RecutReq); rq == null: off
+  RecutReq *rq;
+  uint32_t rq_cap;
+  uint32_t cap_dyn;      // records of a dynamic segment
+  uint64_t *ch_dyn;      // dynamic segment t: start offset | record base << 32, at [end0 + t]
+  unsigned long long *rec_count;  // records allocated (the planner's counter; re-cuts allocate from it too)
+  uint64_t rec_cap;      // records available
+  int32_t recut_idle;    // chains ask for cuts once more waves than this have become helpers
+  uint32_t recut_min;    // ... when at least this many true samples remain
+  float recut_frac[2];   // the new segment starts this fraction of the remainder ahead: [0] lane chains, [1] whole-wave
 };
+
+// ---------------------------------------------------------------- chain segments (planned + dynamic)
+RT_D uint32_t seg_count(const Book1View &V, const ChainPx &P, uint32_t pix) {  // published segments
+  return P.K + (ld_acq(&V.ch_px[pix].kd) & 0xffu);
+}
+RT_D uint64_t dyn_word(const Book1View &V, const ChainPx &P, uint32_t t) { return ld_rel64(&V.ch_dyn[P.end0 + t]); }
+RT_D uint32_t seg_start(const Book1View &V, const ChainPx &P, uint32_t t) {
+  return t < P.K ? t * P.seg_len : (uint32_t)dyn_word(V, P, t);
+}
+RT_D uint32_t seg_cap(const Book1View &V, const ChainPx &P, uint32_t k) {
+  return k + 1u < P.K ? P.cap : k + 1u == P.K ? P.cap_last : V.cap_dyn;
+}
+RT_D uint32_t rec_index(const Book1View &V, const ChainPx &P, uint32_t t, uint32_t c) {
+  return t < P.K ? P.rec0 + (t - 1u) * P.cap + c : (uint32_t)(dyn_word(V, P, t) >> 32) + c;
+}
 
 // ---------------------------------------------------------------- pixel output
 // quantize one pixel (src/raytracing.c:127-131): mean, gamma 2, clamp-macro semantics, truncate
@@ -534,20 +580,22 @@ RT_D bool bf_verify(const float4 *items, const CoopRay &C, float tmin, float bes
 }
 
 // ---------------------------------------------------------------- chain protocol (kMode 2)
-RT_D uint32_t rec_index(const ChainPx &P, uint32_t t, uint32_t c) { return P.rec0 + (t - 1u) * P.cap + c; }
-
 // Coupling scan of chain k at its sample boundary x: does a successor record start at x?  tc = the
-// cursor (successor segment t << 24 | record c), st = the start offset of that record.  Returns true
-// when coupled (tc then names the record that starts at x).  Bounded work per call; a record not yet
-// written, or a successor still running past its last record, is looked at again next time.
-RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t x, uint32_t &tc, uint32_t &st) {
+// cursor (successor segment t << 24 | record c), st = the start offset of that record (kStUnknown: a
+// dynamic successor's start, read once it is published).  Returns true when coupled (tc then names the
+// record that starts at x).  Bounded work per call; a record not yet written, or a successor still
+// running past its last record, is looked at again next time.
+RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t pix, uint32_t x, uint32_t &tc, uint32_t &st) {
   for (int it = 0; it < 24; it++) {
     const uint32_t t = tc >> 24, c = tc & 0xffffffu;
-    if (t >= P.K) return false;  // no successor
-    if (st > x) return false;    // the successor's next sample starts beyond x
+    if (t >= P.K) {  // a dynamic successor -- or none (kNoTarget): published yet?
+      if (t >= P.K + kDynMax || t >= seg_count(V, P, pix)) return false;
+      if (st == kStUnknown) st = seg_start(V, P, t);
+    }
+    if (st > x) return false;  // the successor's next sample starts beyond x
     if (st == x) return true;
-    if (c < seg_cap(P, t)) {  // st < x: step over record c
-      const uint32_t e = ld_rel(&V.ch_end[rec_index(P, t, c)]);
+    if (c < seg_cap(V, P, t)) {  // st < x: step over record c
+      const uint32_t e = ld_rel(&V.ch_end[rec_index(V, P, t, c)]);
       if (e != kRecFill) {
         st = e;
         tc = (t << 24) | (c + 1u);
@@ -562,13 +610,13 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t x, uint32_
       return false;
     }
     const uint32_t t2 = end_t(w), c2 = end_c(w);
-    if (t2 <= t || t2 >= P.K) {  // (never: links point forward)
+    if (t2 <= t || t2 >= P.K + kDynMax) {  // (never: links point forward)
       tc = kNoTarget;
       return false;
     }
-    uint32_t s2 = t2 * P.seg_len;
+    uint32_t s2 = seg_start(V, P, t2);  // (t2 is published: t linked into it)
     if (c2 > 0) {
-      s2 = ld_rel(&V.ch_end[rec_index(P, t2, c2 - 1u)]);
+      s2 = ld_rel(&V.ch_end[rec_index(V, P, t2, c2 - 1u)]);
       if (s2 == kRecFill) return false;
     }
     tc = (t2 << 24) | c2;
@@ -585,7 +633,7 @@ RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint
   if (!(w & kEndEnded)) return false;
   if (w & kEndNoLink) return true;  // segment 0 completed the pixel
   uint32_t total = end_n(w), t = end_t(w), c = end_c(w);
-  for (uint32_t it = 0; it < P.K; it++) {
+  for (uint32_t it = 0; it < P.K + kDynMax; it++) {
     if (t == k) return total + (n - c) >= spp;
     if (t > k) return true;  // the true chain skips this chain
     w = ld_rel64(&V.ch_seg[P.end0 + t]);
@@ -593,6 +641,27 @@ RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint
     if (w & kEndNoLink) return true;  // the true chain ends (or breaks) before this chain
     total += end_n(w) - c;
     if (total >= spp) return true;
+    t = end_t(w), c = end_c(w);
+  }
+  return false;
+}
+
+// The true samples the links cover before chain k's link point (record c_at of k), when every chain
+// before k has ended and the true chain reaches k; false otherwise (undecided, or k is not needed).
+RT_D bool chain_covered(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t &total, uint32_t &c_at) {
+  uint64_t w = ld_rel64(&V.ch_seg[P.end0]);
+  if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
+  total = end_n(w);
+  uint32_t t = end_t(w), c = end_c(w);
+  for (uint32_t it = 0; it < P.K + kDynMax; it++) {
+    if (t == k) {
+      c_at = c;
+      return true;
+    }
+    if (t > k) return false;
+    w = ld_rel64(&V.ch_seg[P.end0 + t]);
+    if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
+    total += end_n(w) - c;
     t = end_t(w), c = end_c(w);
   }
   return false;
@@ -635,18 +704,18 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
     }
     return true;
   }
-  if (k > 0 && s >= seg_cap(P, k)) {  // the list is full
+  if (k > 0 && s >= seg_cap(V, P, k)) {  // the list is full
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
-  if (chain_couple(V, P, x, tc, st)) {
+  if (chain_couple(V, P, (uint32_t)pix, x, tc, st)) {
     if (writer) {
       if (k == 0) V.ch_acc0[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
       st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc));
     }
     return true;
   }
-  if (k > 0 && s >= P.check && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
+  if (k > 0 && s >= (k < P.K ? P.check : 0u) && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
@@ -656,9 +725,131 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
 // Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it).
 RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, f3 col, uint32_t x_end) {
   const ChainPx &P = V.ch_px[pix];
-  const uint32_t at = rec_index(P, k, c);
+  const uint32_t at = rec_index(V, P, k, c);
   V.ch_col[at] = make_float4(col.x, col.y, col.z, u2f(x_end));
   st_rel(&V.ch_end[at], x_end);
+}
+
+// A chain's start: stream position, and its coupling cursor (its planned successor; a last segment
+// has none until it asks for a cut).
+RT_D void chain_start(const Book1View &V, uint32_t pix, uint32_t seg, Pcg32 &g, uint32_t &tc, uint32_t &st) {
+  const ChainPx &P = V.ch_px[pix];
+  g.skip(seg_start(V, P, seg));
+  tc = kNoTarget;
+  st = 0u;
+  if (seg + 1u < P.K) tc = (seg + 1u) << 24, st = (seg + 1u) * P.seg_len;
+}
+
+// ---------------------------------------------------------------- run-time re-cut (RecutReq)
+// May this chain ask for a cut?  A segment >= 1 without a successor (a planned last segment, or a
+// dynamic one) whose cursor is free; the helper re-checks that it is still the pixel's last.
+RT_D bool recut_candidate(uint32_t seg, uint32_t tc) { return !(seg & kItemUnsplit) && seg > 0u && tc == kNoTarget; }
+
+// Wave helpers that also compile for the host-side protocol simulator (tests/native/chain_sim.cpp),
+// where a "wave" is one thread.
+RT_D uint32_t wv_lane() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__lane_id();
+#else
+  return 0u;
+#endif
+}
+RT_D uint32_t wv_width() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return 64u;
+#else
+  return 1u;
+#endif
+}
+RT_D uint32_t wv_first(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+#else
+  return v;
+#endif
+}
+RT_D void wv_fence_release() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+  __atomic_thread_fence(__ATOMIC_RELEASE);
+#endif
+}
+RT_D uint32_t at_add(uint32_t *p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RT_D bool at_cas(uint32_t *p, uint32_t expect, uint32_t v) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// True samples the pixel still needs beyond chain k's s records, once the links before k are decided
+// (else 0): what a cut of k would share out.
+RT_D uint32_t recut_left(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t s) {
+  uint32_t total = 0u, c_at = 0u;
+  if (!chain_covered(V, P, k, total, c_at)) return 0u;
+  const uint32_t mine = s > c_at ? s - c_at : 0u;
+  const uint32_t spp = (uint32_t)V.S.cam.spp;
+  return total + mine < spp ? spp - total - mine : 0u;
+}
+
+// Ask (one writer lane): enqueue the request and point the cursor at the successor to come.
+RT_D void recut_request(const Book1View &V, uint32_t pix, uint32_t seg, uint32_t x, uint32_t s, bool wave, bool writer,
+                        uint32_t &tc, uint32_t &st) {
+  if (writer) {
+    const uint32_t idx = at_add(&V.mig[kMigRqPush], 1u);
+    if (idx < V.rq_cap) {
+      RecutReq &r = V.rq[idx];
+      r.pix = pix, r.seg = seg, r.x = x, r.s = s, r.wave = wave ? 1u : 0u;
+      __hip_atomic_store(&r.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  tc = (seg + 1u) << 24;  // (a request the helpers never act on leaves the chain as it was: no successor)
+  st = kStUnknown;
+}
+
+// Publish a cut for request r (wave-uniform: every lane calls; lane 0 decides and stores, the wave
+// fills the new record list).  Returns the new segment t >= 1 to run, or 0 when the request is stale
+// (the chain is no longer the last, has ended, the links before it are undecided) or not worth it.
+RT_D uint32_t recut_publish(const Book1View &V, const RecutReq &r) {
+  const bool l0 = wv_lane() == 0u;
+  const ChainPx P = V.ch_px[r.pix];
+  uint32_t *kdp = (uint32_t *)&V.ch_px[r.pix].kd;
+  uint32_t t = 0u, x_new = 0u, kd = 0u, base = 0u;
+  if (l0) {
+    kd = ld_acq(kdp);
+    const uint32_t tn = P.K + (kd & 0xffu);
+    const bool last = !(kd & 0x100u) && r.seg + 1u == tn && tn < P.K + kDynMax && tn < (uint32_t)kMaxSeg && r.s > 0u;
+    const uint64_t w = last ? ld_rel64(&V.ch_seg[P.end0 + r.seg]) : kEndEnded;
+    const uint32_t left = (w & kEndEnded) ? 0u : recut_left(V, P, r.seg, r.s);
+    if (left > 0u) {
+      const float per = (float)(r.x - seg_start(V, P, r.seg)) / (float)r.s;  // its draws per sample
+      const float ahead = V.recut_frac[r.wave ? 1 : 0] * (float)left * per;
+      const uint32_t dx = ((uint32_t)fminf(ahead, 1e9f) + 1u) & ~1u;
+      x_new = r.x + (dx > 2u ? dx : 2u);
+      if (left >= V.recut_min && x_new > r.x && x_new < 0x3fffffffu && at_cas(kdp, kd, kd | 0x100u)) {  // lock
+        const unsigned long long b =
+            __hip_atomic_fetch_add(V.rec_count, (unsigned long long)V.cap_dyn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (b + V.cap_dyn <= V.rec_cap && b + V.cap_dyn <= 0xffffffffull) {
+          t = tn;
+          base = (uint32_t)b;
+        } else {
+          st_rel(kdp, kd);  // out of records: unlock, no cut
+        }
+      }
+    }
+  }
+  t = wv_first(t);
+  if (t == 0u) return 0u;
+  base = wv_first(base);
+  for (uint32_t q = wv_lane(); q < V.cap_dyn; q += wv_width()) st_rel(&V.ch_end[base + q], kRecFill);
+  wv_fence_release();  // (every lane: its fills before the words that publish them)
+  if (l0) {
+    st_rel64(&V.ch_seg[P.end0 + t], 0ull);
+    st_rel64(&V.ch_dyn[P.end0 + t], ((uint64_t)base << 32) | x_new);
+    __hip_atomic_store(kdp, (kd & 0xffu) + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // publish t
+  }
+  return t;
 }
 
 // ---------------------------------------------------------------- whole-wave work items
@@ -666,9 +857,11 @@ RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, 
 // values and runs the same shading), and each ray is traced by the wave (bf_candidate + bf_verify,
 // or the exact scan).  The item is a whole pixel (kMode 0: its samples in order), or a chain
 // (kMode 2: segment / unsplit pixel, with the same boundary protocol as a lane).
+// tail: the launch's tail is known to have begun (a helper runs this item): a last segment asks for a
+// cut at once; otherwise it checks the helper count every ~20 us.
 template <int kMode>
 RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix, uint32_t seg,
-                           uint8_t *__restrict__ out, const MigRec *res = nullptr) {
+                           uint8_t *__restrict__ out, const MigRec *res = nullptr, bool tail = false) {
   const rt_camera &cam = V.S.cam;
   const int W = cam.width;
   const int jj = (int)(pix / W);
@@ -687,10 +880,9 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     s = res->s, tc = res->tc, st = res->st;
     acc = mk(res->acc[0], res->acc[1], res->acc[2]);
   } else if (kMode == 2 && !(seg & kItemUnsplit)) {
-    const ChainPx &P = V.ch_px[pix];
-    g.skip(seg * P.seg_len);
-    if (seg + 1u < P.K) tc = (seg + 1u) << 24, st = (seg + 1u) * P.seg_len;
+    chain_start(V, (uint32_t)pix, seg, g, tc, st);
   }
+  uint64_t gate_next = 0;
   const bool use_bf = V.n_bf_leaves > 0;
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
   if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
@@ -700,6 +892,15 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
       if (__builtin_amdgcn_readfirstlane((int)done)) break;
+      if (V.rq && recut_candidate(seg, tc)) {  // a last segment in the launch's tail: ask for a cut
+        if (!tail && wall_clock64() >= gate_next) {
+          tail = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.recut_idle;
+          tail = __builtin_amdgcn_readfirstlane((int)tail);
+          gate_next = wall_clock64() + 2000u;
+        }
+        if (tail && recut_left(V, V.ch_px[pix], seg, s) >= V.recut_min)
+          recut_request(V, (uint32_t)pix, seg, g.n, s, true, lane0, tc, st);
+      }
     } else if (s == (uint32_t)cam.spp) {
       break;
     }
@@ -866,6 +1067,45 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
       continue;
     }
     if (__builtin_amdgcn_readfirstlane(fin)) break;
+    // Nothing migrated to run: a re-cut request?  The helper first takes back its credit (so no lane
+    // queues an item to it while it runs a segment), and gives it again afterwards.
+    if (V.rq) {
+      int req = -1;
+      if (l0) {
+        const uint32_t p = ld_rel(&V.mig[kMigRqPop]);
+        uint32_t q = ld_rel(&V.mig[kMigRqPush]);
+        q = q < V.rq_cap ? q : V.rq_cap;
+        if (p < q) {
+          uint32_t c = ld_rel(box + kMigCredits);
+          bool mine = false;
+          while ((int32_t)c > 0 && !mine) {
+            const uint32_t prev = atomicCAS(box + kMigCredits, c, c - 1u);
+            mine = prev == c;
+            c = prev;
+          }
+          if (mine) {
+            if (atomicCAS(&V.mig[kMigRqPop], p, p + 1u) == p) req = (int)p;
+            else atomicAdd(box + kMigCredits, 1u);
+          }
+        }
+      }
+      req = __builtin_amdgcn_readfirstlane(req);
+      if (req >= 0) {
+        const RecutReq *rp = &V.rq[(uint32_t)req];
+        while (__hip_atomic_load(&rp->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != V.mig_epoch)
+          __builtin_amdgcn_s_sleep(1);
+        const RecutReq r = *rp;
+        const uint32_t t = recut_publish(V, r);
+        if (t) {
+          __builtin_amdgcn_s_setprio(2);
+          render_item_coop<kMode>(V, items9, (int64_t)wv_first(r.pix), t, out, nullptr, true);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        if (l0) atomicAdd(box + kMigCredits, 1u);
+        idle_since = wall_clock64();
+        continue;
+      }
+    }
     // A helper idle for mig_wait leaves -- but only by taking back a credit that no push has claimed.
     // A claimed credit stands for an item that is (being) queued in this mailbox, which then still
     // has a helper to run it; so no item is ever queued to a mailbox whose helpers have all left.
@@ -993,6 +1233,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
   uint64_t mig_next = 0;
+  bool recut_ok = false;   // re-cut gate (wave-uniform), likewise
+  uint64_t recut_next = 0;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
   int32_t pix = 0;  // (< 2^31: host-checked)
@@ -1068,6 +1310,16 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
       }
       mig_try = mig_ok;
+    }
+    // run-time re-cut: once more than recut_idle waves have become helpers, a last segment asks for a
+    // cut (RecutReq); the same rare read of the helper count, only by waves holding such a chain
+    if (kMode == 2 && V.rq && !recut_ok && __ballot(recut_candidate(seg, tc)) != 0) {
+      const uint64_t now = wall_clock64();
+      if (now >= recut_next) {
+        recut_ok = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.recut_idle;
+        recut_ok = __builtin_amdgcn_readfirstlane((int)recut_ok);
+        recut_next = now + 2000u;
+      }
     }
     // ---------------- shading pass (Camera_ray_color body after hit(), src/raytracing.c:44-75)
     bool need_pixel = !have_result, need_sample = false;
@@ -1153,9 +1405,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (kMode == 2 && cont) {
           g.skip(st);
         } else if (kMode == 2 && !(seg & kItemUnsplit)) {
-          const ChainPx &P = V.ch_px[pix];
-          g.skip(seg * P.seg_len);
-          if (seg + 1u < P.K) tc = (seg + 1u) << 24, st = (seg + 1u) * P.seg_len;
+          chain_start(V, (uint32_t)pix, seg, g, tc, st);
         }
         need_pixel = false;
         px_steps = 0;
@@ -1167,6 +1417,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         need_pixel = true;  // this item is finished
         continue;
       }
+      if (kMode == 2 && recut_ok && (s & 3) == 0 && recut_candidate(seg, tc) &&
+          recut_left(V, V.ch_px[pix], seg, (uint32_t)s) >= V.recut_min)
+        recut_request(V, (uint32_t)pix, seg, g.n, (uint32_t)s, false, true, tc, st);
       if (mig_try && !need_pixel && mig_push(V, (uint32_t)glane % kMigBoxes, pix, seg, (uint32_t)s, acc, g, tc, st)) {
         mode = kExit;  // handed over at this sample boundary
         need_sample = false;
@@ -1261,16 +1514,16 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     acc = mk(a0.x, a0.y, a0.z);
     total = end_n(w);
     t = end_t(w), c = end_c(w);
-    o = c == 0 ? t * P.seg_len : V.ch_end[rec_index(P, t, c - 1u)];
+    o = c == 0 ? seg_start(V, P, t) : V.ch_end[rec_index(V, P, t, c - 1u)];
   }
   while (linked && total < spp) {
-    if (t == 0 || t >= P.K) break;  // (never: links point forward)
+    if (t == 0 || t >= P.K + kDynMax) break;  // (never: links point forward)
     w = V.ch_seg[P.end0 + t];
     const uint32_t n = end_n(w);
     const uint32_t m = n > c ? min(n - c, spp - total) : 0u;
     for (uint32_t b = 0; b < m; b += 64) {
       float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (b + (uint32_t)lane < m) r = V.ch_col[rec_index(P, t, c + b + (uint32_t)lane)];
+      if (b + (uint32_t)lane < m) r = V.ch_col[rec_index(V, P, t, c + b + (uint32_t)lane)];
       const uint32_t cnt = min(64u, m - b);
       for (uint32_t q = 0; q < cnt; q++)
         acc = add(acc, mk(lane_bcast(r.x, (int)q), lane_bcast(r.y, (int)q), lane_bcast(r.z, (int)q)));

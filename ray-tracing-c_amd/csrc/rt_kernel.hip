@@ -460,8 +460,10 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       const uint32_t need = (uint32_t)(K - 2) * cap + cap_last;
       const unsigned long long r0 = atomicAdd((unsigned long long *)&cnt[kCnRec], (unsigned long long)need);
       const bool fits = r0 + need <= (unsigned long long)m.rec_cap;
-      const uint32_t e0 = fits ? atomicAdd(&cnt[kCnSeg], (uint32_t)K) : 0xffffffffu;
-      if (!fits || (uint64_t)e0 + (uint32_t)K > (uint64_t)m.seg_cap) {
+      // end words: K planned segments + kDynMax dynamic ones (run-time re-cut)
+      const uint32_t n_end = (uint32_t)K + b1::kDynMax;
+      const uint32_t e0 = fits ? atomicAdd(&cnt[kCnSeg], n_end) : 0xffffffffu;
+      if (!fits || (uint64_t)e0 + n_end > (uint64_t)m.seg_cap) {
         K = 1;  // out of record / end-word space: this pixel stays whole (the reservation is left unused)
       } else {
         b1::ChainPx P;
@@ -472,9 +474,9 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
         P.end0 = e0;
         P.check = (uint32_t)(3 * (m.spp / K) / 4);
         P.cap_last = cap_last;
-        P.pad = 0u;
+        P.kd = 0u;
         px[p] = P;
-        for (int k = 0; k < K; k++) seg[e0 + k] = 0ull;
+        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull;
         split[atomicAdd(&cnt[kCnSplit], 1u)] = (uint32_t)p;
       }
     }
@@ -633,6 +635,10 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
+  bool recut = true;  // run-time re-cut of last segments (rt_book1.h: RecutReq)
+  int recut_idle = 25;     //   once this percentage of the grid's waves has become helpers
+  int recut_min = 32;      //   for chains with at least this many true samples left
+  float recut_frac_lane = 0.3f, recut_frac_wave = 0.5f;  //   the new segment starts this share of them ahead
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
   int lane_occ = 5;   // lane kernel occupancy target
   int sample_cost = 0;     // cost pre-pass: per-sample latency in traversal steps (measured: 75-250 slower; off)
@@ -651,6 +657,11 @@ struct Config {
     c.mig_wait_us = env_int("RT_MIG_WAIT_US", c.mig_wait_us);
     if (c.mig_wait_us < 0) c.mig_wait_us = 0;
     c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
+    c.recut = env_flag("RT_RECUT", c.recut);
+    c.recut_idle = env_int("RT_RECUT_IDLE", c.recut_idle);
+    c.recut_min = env_int("RT_RECUT_MIN", c.recut_min);
+    if (c.recut_min < 2) c.recut_min = 2;
+    if (const char *e = getenv("RT_RECUT_FRAC")) sscanf(e, "%f,%f", &c.recut_frac_lane, &c.recut_frac_wave);
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
@@ -749,6 +760,9 @@ struct rt_device_scene {
   float4 *ch_acc0 = nullptr;
   b1::ChainCont *ch_cont = nullptr;
   uint32_t ch_seg_cap = 0;
+  uint64_t *ch_dyn = nullptr;       // dynamic segments' start / record base (run-time re-cut)
+  b1::RecutReq *rq = nullptr;       // re-cut request queue
+  uint32_t rq_cap = 0;
   void *ch_rec_arena = nullptr;
   size_t ch_rec_cap = 0;  // records
   // general path (rt_general.h) for scenes outside the Book-1 path
@@ -1160,13 +1174,15 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   // chain scratch for the whole frame (a launch covers at most every pixel)
   {
     const int kmax = cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave;
-    const size_t nseg = npix * (size_t)kmax;
+    const size_t nitem = npix * (size_t)kmax, nseg = npix * (size_t)(kmax + b1::kDynMax);
     d->ch_seg_cap = nseg < 0xffffffffu ? (uint32_t)nseg : 0xffffffffu;
-    const size_t cs[9] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
-                          npix * sizeof(b1::ChainPx), nseg * sizeof(uint2), nseg * sizeof(uint64_t),
-                          nseg * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont)};
-    size_t co[9], ct = 0;
-    for (int k = 0; k < 9; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
+    d->rq_cap = (uint32_t)(2 * npix + 4096 < 0x7fffffffu ? 2 * npix + 4096 : 0x7fffffffu);
+    const size_t cs[11] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
+                           npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
+                           nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont),
+                           nseg * sizeof(uint64_t), (size_t)d->rq_cap * sizeof(b1::RecutReq)};
+    size_t co[11], ct = 0;
+    for (int k = 0; k < 11; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
     HIP_OK(hipMalloc(&d->ch_arena, ct));
     char *c = (char *)d->ch_arena;
     d->ch_cnt = (uint32_t *)(c + co[0]);
@@ -1178,6 +1194,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_wave_key = (uint64_t *)(c + co[6]);
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
+    d->ch_dyn = (uint64_t *)(c + co[9]);
+    d->rq = (b1::RecutReq *)(c + co[10]);
     if (cfg.px_time) {
       HIP_OK(hipMalloc(&d->seg_time, nseg * 2 * sizeof(uint32_t)));
       V.seg_time = d->seg_time;
@@ -1515,6 +1533,18 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
+  V.ch_dyn = d->ch_dyn;
+  V.rec_count = (unsigned long long *)(d->ch_cnt + kCnRec);
+  V.rec_cap = d->ch_rec_cap;
+  V.cap_dyn = (uint32_t)V.S.cam.spp + (uint32_t)cfg.chain_slack;
+  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // (helpers run the cuts: they need migration + the LDS scene)
+    V.rq = d->rq;
+    V.rq_cap = d->rq_cap;
+    V.recut_idle = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.recut_idle / 100);
+    V.recut_min = (uint32_t)cfg.recut_min;
+    V.recut_frac[0] = cfg.recut_frac_lane;
+    V.recut_frac[1] = cfg.recut_frac_wave;
+  }
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
@@ -1549,6 +1579,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   // continuation items (normally none: the launch exits at once)
   b1::Book1View C = V;
   C.n_coop = nullptr;
+  C.rq = nullptr;  // (continuation items are whole pixels: nothing to cut)
   C.ch_cont = d->ch_cont;
   C.ch_n_cont = d->ch_cnt + kCnCont;
   C.mig_epoch = ++d->mig_epoch;

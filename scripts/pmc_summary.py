@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--stats-frames", type=int, default=1)
     ap.add_argument("--pmc-frames", type=int, default=1)
     ap.add_argument("pmc", nargs="*")
-    a = ap.parse_args()
+    a = ap.parse_intermixed_args()
     res = collections.defaultdict(dict)
     if a.stats:
         for f in glob.glob(f"{a.stats}/**/*kernel_stats.csv", recursive=True):
@@ -48,6 +48,11 @@ def main():
                 e["calls"] = int(r["Calls"])
                 e["total_ns"] = float(r["TotalDurationNs"])
                 e["kernel_ms_per_frame"] = float(r["TotalDurationNs"]) / a.stats_frames / 1e6
+        for f in glob.glob(f"{a.stats}/**/*kernel_trace.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Kernel_Name"] in res:  # every dispatch's duration (ms), in order
+                    res[r["Kernel_Name"]].setdefault("dispatch_ms", []).append(
+                        round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, 4))
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for d in a.pmc:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):

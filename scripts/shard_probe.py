@@ -29,6 +29,7 @@ def time_rows(row0, stride, n, reps=2):
         ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()
         best = min(best, time.perf_counter() - t0)
+        ds.check()  # every work item finished
         kbest = min(kbest, ds.last_launch_ms())
     last = buf.cpu().numpy()
     return best, kbest
