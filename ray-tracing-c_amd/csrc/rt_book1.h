@@ -69,22 +69,27 @@ struct ChainPx {       // 32 B per pixel of a chain launch (chain_plan_kernel)
   uint32_t kd;         // run-time re-cut (RecutReq): dynamic segments published (low 8 bits; atomic);
                        // bit 8 while one is being published
 };
-// Run-time re-cut.  The last segment of a pixel absorbs the whole error of the planner's stream
-// length estimate (the tail of an N-GPU share: DESIGN.md §5).  Once the launch has idle helper waves,
-// a running last segment k asks for a cut (RecutReq); a helper appends segment t = k + 1 at an offset
-// ahead of k -- the remaining true samples R (exact: spp minus what the links already cover) times the
-// chain's own draws per sample, times a fraction -- with a record list of its own, publishes it
-// (ChainPx.kd) and runs it.  Segment k then couples into t exactly like into a planned successor, and
-// t, now the last, may be cut again.  Segments stay ordered by start offset, so links still point
-// forward and the fold is unchanged.  Dynamic segment t (K <= t < K + kDynMax) has its start offset
-// and record base in ch_dyn[end0 + t]; its end word is ch_seg[end0 + t] (the planner reserves
-// K + kDynMax end words per split pixel).
+// Run-time re-cut.  Once a launch's work items are all handed out (its tail), a chain with much of
+// its stream left asks for a cut (RecutReq): a lane that found no item left (or an idle helper wave)
+// inserts a dynamic segment t right after the chain's segment k, at an offset ahead of it -- a fraction
+// of the draws between k's position and the start of k's successor (for a last segment: of the
+// stream's remaining true samples times the chain's draws per sample) -- with a record list of its
+// own, and runs it.  Segment k, watching its successor word since it asked, couples into t exactly as
+// into a planned successor, and t couples into k's old successor.  Segments stay ordered by start
+// offset (links point forward in offset), so the fold is unchanged.  Per segment slot end0 + t
+// (t < K + kDynMax; the planner reserves the slots): the end word ch_seg, and SegDyn: a dynamic
+// segment's start, record base and capacity, and for every segment its successor once a cut changed it.
 constexpr uint32_t kDynMax = 8;
-constexpr uint32_t kStUnknown = 0xffffffffu;  // coupling cursor on a dynamic successor whose start is not read yet
-struct RecutReq {      // 32 B: a last segment asking to be cut (pushed by its lane / helper wave)
+constexpr uint32_t kNone = 0xffu;  // no successor
+struct SegDyn {        // 16 B per segment slot
+  uint32_t start, base, cap;  // a dynamic segment: stream offset, first record, records
+  uint32_t next;              // 0: the planned successor (t + 1 < K ? t + 1 : none); else successor + 1
+};
+struct RecutReq {      // 32 B: a chain asking to be cut (pushed by its lane / helper wave)
   uint32_t pix, seg;
-  uint32_t x, s;       // the chain's stream offset and records at the request
-  uint32_t wave;       // 1: the chain runs on a whole wave (fast), 0: in a lane
+  uint32_t x_new;      // the new segment's start offset
+  uint32_t next;       // k's successor when it asked (the cut is stale if that changed)
+  uint32_t cap;        // records for the new segment
   uint32_t ready;      // the launch's epoch, written last (release)
   uint32_t pad[2];
 };
@@ -195,28 +200,30 @@ struct Book1View {
   // run-time re-cut (RecutReq); rq == null: off
   RecutReq *rq;
   uint32_t rq_cap;
-  uint32_t cap_dyn;      // records of a dynamic segment
-  uint64_t *ch_dyn;      // dynamic segment t: start offset | record base << 32, at [end0 + t]
-  unsigned long long *rec_count;  // records allocated (the planner's counter; re-cuts allocate from it too)
-  uint64_t rec_cap;      // records available
-  int32_t recut_idle;    // chains ask for cuts once more waves than this have become helpers
-  uint32_t recut_min;    // ... when at least this many true samples remain
-  float recut_frac[2];   // the new segment starts this fraction of the remainder ahead: [0] lane chains, [1] whole-wave
+  SegDyn *ch_sd;         // per segment slot [end0 + t]
+  unsigned long long *rec_count;  // records allocated (the planner's counter; cuts allocate from it too)
+  const uint32_t *rec_filled;     // records whose end word holds kRecFill (chain_fill_kernel): cuts stay below
+  uint32_t recut_min;    // a chain asks when at least this many of its samples remain
+  float recut_frac;      // the cut keeps this share of the chain's remaining draws on the chain
+  uint32_t recut_slack;  // records of a dynamic segment: 2 x its share of samples + this
+  uint32_t *recut_stats; // diagnostics (accumulated per scene): [0] cuts published, [1] requests declined
 };
 
 // ---------------------------------------------------------------- chain segments (planned + dynamic)
-RT_D uint32_t seg_count(const Book1View &V, const ChainPx &P, uint32_t pix) {  // published segments
-  return P.K + (ld_acq(&V.ch_px[pix].kd) & 0xffu);
-}
-RT_D uint64_t dyn_word(const Book1View &V, const ChainPx &P, uint32_t t) { return ld_rel64(&V.ch_dyn[P.end0 + t]); }
+RT_D uint32_t ld_sd(const uint32_t &w) { return ld_rel(&w); }
 RT_D uint32_t seg_start(const Book1View &V, const ChainPx &P, uint32_t t) {
-  return t < P.K ? t * P.seg_len : (uint32_t)dyn_word(V, P, t);
+  return t < P.K ? t * P.seg_len : ld_sd(V.ch_sd[P.end0 + t].start);
 }
 RT_D uint32_t seg_cap(const Book1View &V, const ChainPx &P, uint32_t k) {
-  return k + 1u < P.K ? P.cap : k + 1u == P.K ? P.cap_last : V.cap_dyn;
+  return k + 1u < P.K ? P.cap : k + 1u == P.K ? P.cap_last : ld_sd(V.ch_sd[P.end0 + k].cap);
 }
 RT_D uint32_t rec_index(const Book1View &V, const ChainPx &P, uint32_t t, uint32_t c) {
-  return t < P.K ? P.rec0 + (t - 1u) * P.cap + c : (uint32_t)(dyn_word(V, P, t) >> 32) + c;
+  return t < P.K ? P.rec0 + (t - 1u) * P.cap + c : ld_sd(V.ch_sd[P.end0 + t].base) + c;
+}
+RT_D uint32_t seg_next(const Book1View &V, const ChainPx &P, uint32_t t) {  // successor segment, or kNone
+  const uint32_t v = V.ch_sd ? ld_acq(&V.ch_sd[P.end0 + t].next) : 0u;
+  if (v) return v - 1u;
+  return t + 1u < P.K ? t + 1u : kNone;
 }
 
 // ---------------------------------------------------------------- pixel output
@@ -580,25 +587,33 @@ RT_D bool bf_verify(const float4 *items, const CoopRay &C, float tmin, float bes
 }
 
 // ---------------------------------------------------------------- chain protocol (kMode 2)
+// Coupling cursor: successor segment t << 24 | flags | record c.  kWatch: the chain has asked for a cut
+// and reads its successor word until a new successor shows up; kNoAsk: it never asks (too little left).
+constexpr uint32_t kWatch = 0x800000u, kNoAsk = 0x400000u, kCurRec = 0x3fffffu;
+
 // Coupling scan of chain k at its sample boundary x: does a successor record start at x?  tc = the
-// cursor (successor segment t << 24 | record c), st = the start offset of that record (kStUnknown: a
-// dynamic successor's start, read once it is published).  Returns true when coupled (tc then names the
-// record that starts at x).  Bounded work per call; a record not yet written, or a successor still
-// running past its last record, is looked at again next time.
-RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t pix, uint32_t x, uint32_t &tc, uint32_t &st) {
-  for (int it = 0; it < 24; it++) {
-    const uint32_t t = tc >> 24, c = tc & 0xffffffu;
-    if (t >= P.K) {  // a dynamic successor -- or none (kNoTarget): published yet?
-      if (t >= P.K + kDynMax || t >= seg_count(V, P, pix)) return false;
-      if (st == kStUnknown) st = seg_start(V, P, t);
+// cursor, st = the start offset of its record.  Returns true when coupled (tc then names the record
+// that starts at x).  Bounded work per call; a record not yet written, or a successor still running
+// past its last record, is looked at again next time.
+RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t x, uint32_t &tc, uint32_t &st) {
+  if (tc & kWatch) {  // asked for a cut: a new successor?  (switch only if it starts ahead of this chain)
+    const uint32_t n = seg_next(V, P, k);
+    if (n != (tc >> 24)) {
+      const uint32_t sn = seg_start(V, P, n);
+      if (sn > x) tc = n << 24, st = sn;
+      else tc &= ~kWatch;  // (it landed behind this chain: ignore it, it couples into the old successor)
     }
+  }
+  for (int it = 0; it < 24; it++) {
+    const uint32_t t = tc >> 24, c = tc & kCurRec;
+    if (t >= P.K + kDynMax) return false;  // no successor (kNoTarget)
     if (st > x) return false;  // the successor's next sample starts beyond x
     if (st == x) return true;
     if (c < seg_cap(V, P, t)) {  // st < x: step over record c
       const uint32_t e = ld_rel(&V.ch_end[rec_index(V, P, t, c)]);
       if (e != kRecFill) {
         st = e;
-        tc = (t << 24) | (c + 1u);
+        tc = (tc & ~kCurRec) | (c + 1u);
         continue;
       }
     }
@@ -606,20 +621,20 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t pix, uint3
     const uint64_t w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded) || c < end_n(w)) return false;  // running, or its record c still in flight
     if (w & kEndNoLink) {
-      tc = kNoTarget;  // it ended without a link: nothing to couple with beyond it
+      tc = kNoTarget | (tc & kNoAsk);  // it ended without a link: nothing to couple with beyond it
       return false;
     }
     const uint32_t t2 = end_t(w), c2 = end_c(w);
-    if (t2 <= t || t2 >= P.K + kDynMax) {  // (never: links point forward)
-      tc = kNoTarget;
+    if (t2 == t || t2 >= P.K + kDynMax) {  // (never: links point forward)
+      tc = kNoTarget | (tc & kNoAsk);
       return false;
     }
-    uint32_t s2 = seg_start(V, P, t2);  // (t2 is published: t linked into it)
+    uint32_t s2 = seg_start(V, P, t2);
     if (c2 > 0) {
       s2 = ld_rel(&V.ch_end[rec_index(V, P, t2, c2 - 1u)]);
       if (s2 == kRecFill) return false;
     }
-    tc = (t2 << 24) | c2;
+    tc = (t2 << 24) | (tc & kNoAsk) | c2;  // (a followed link ends any watch: the cut, if one comes, is behind)
     st = s2;
   }
   return false;
@@ -627,15 +642,16 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t pix, uint3
 
 // Does chain k (holding n records) still have work?  Follows the links from segment 0: returns true
 // (stop) when the pixel's spp true samples are already covered up to this chain's records, or when
-// the true chain provably never reaches this chain; false while that is undecided.
+// the true chain provably never reaches this chain (it jumps past k's start); false while undecided.
 RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t n, uint32_t spp) {
   uint64_t w = ld_rel64(&V.ch_seg[P.end0]);
   if (!(w & kEndEnded)) return false;
   if (w & kEndNoLink) return true;  // segment 0 completed the pixel
   uint32_t total = end_n(w), t = end_t(w), c = end_c(w);
+  const uint32_t sk = seg_start(V, P, k);
   for (uint32_t it = 0; it < P.K + kDynMax; it++) {
     if (t == k) return total + (n - c) >= spp;
-    if (t > k) return true;  // the true chain skips this chain
+    if (seg_start(V, P, t) > sk) return true;  // the true chain skips this chain
     w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded)) return false;
     if (w & kEndNoLink) return true;  // the true chain ends (or breaks) before this chain
@@ -653,12 +669,13 @@ RT_D bool chain_covered(const Book1View &V, const ChainPx &P, uint32_t k, uint32
   if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
   total = end_n(w);
   uint32_t t = end_t(w), c = end_c(w);
+  const uint32_t sk = seg_start(V, P, k);
   for (uint32_t it = 0; it < P.K + kDynMax; it++) {
     if (t == k) {
       c_at = c;
       return true;
     }
-    if (t > k) return false;
+    if (seg_start(V, P, t) > sk) return false;
     w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
     total += end_n(w) - c;
@@ -708,10 +725,10 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
-  if (chain_couple(V, P, (uint32_t)pix, x, tc, st)) {
+  if (chain_couple(V, P, k, x, tc, st)) {
     if (writer) {
       if (k == 0) V.ch_acc0[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-      st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc));
+      st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc & ~(kWatch | kNoAsk)));
     }
     return true;
   }
@@ -730,21 +747,20 @@ RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, 
   st_rel(&V.ch_end[at], x_end);
 }
 
-// A chain's start: stream position, and its coupling cursor (its planned successor; a last segment
-// has none until it asks for a cut).
+// A chain's start: stream position, and its coupling cursor on its successor.
 RT_D void chain_start(const Book1View &V, uint32_t pix, uint32_t seg, Pcg32 &g, uint32_t &tc, uint32_t &st) {
   const ChainPx &P = V.ch_px[pix];
   g.skip(seg_start(V, P, seg));
-  tc = kNoTarget;
-  st = 0u;
-  if (seg + 1u < P.K) tc = (seg + 1u) << 24, st = (seg + 1u) * P.seg_len;
+  const uint32_t n = seg_next(V, P, seg);
+  tc = n << 24;  // (kNone << 24 == kNoTarget)
+  st = n == kNone ? 0u : seg_start(V, P, n);
+}
+// A dynamic segment (a cut): not one of the launch's work items.
+RT_D bool seg_dynamic(const Book1View &V, uint32_t pix, uint32_t seg) {
+  return !(seg & kItemUnsplit) && seg >= V.ch_px[pix].K;
 }
 
 // ---------------------------------------------------------------- run-time re-cut (RecutReq)
-// May this chain ask for a cut?  A segment >= 1 without a successor (a planned last segment, or a
-// dynamic one) whose cursor is free; the helper re-checks that it is still the pixel's last.
-RT_D bool recut_candidate(uint32_t seg, uint32_t tc) { return !(seg & kItemUnsplit) && seg > 0u && tc == kNoTarget; }
-
 // Wave helpers that also compile for the host-side protocol simulator (tests/native/chain_sim.cpp),
 // where a "wave" is one thread.
 RT_D uint32_t wv_lane() {
@@ -754,25 +770,11 @@ RT_D uint32_t wv_lane() {
   return 0u;
 #endif
 }
-RT_D uint32_t wv_width() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return 64u;
-#else
-  return 1u;
-#endif
-}
 RT_D uint32_t wv_first(uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 #else
   return v;
-#endif
-}
-RT_D void wv_fence_release() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#else
-  __atomic_thread_fence(__ATOMIC_RELEASE);
 #endif
 }
 RT_D uint32_t at_add(uint32_t *p, uint32_t v) {
@@ -784,72 +786,106 @@ RT_D bool at_cas(uint32_t *p, uint32_t expect, uint32_t v) {
 }
 
 // True samples the pixel still needs beyond chain k's s records, once the links before k are decided
-// (else 0): what a cut of k would share out.
+// (else kLeftUnknown).
+constexpr uint32_t kLeftUnknown = 0xffffffffu;
 RT_D uint32_t recut_left(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t s) {
   uint32_t total = 0u, c_at = 0u;
-  if (!chain_covered(V, P, k, total, c_at)) return 0u;
+  if (!chain_covered(V, P, k, total, c_at)) return kLeftUnknown;
   const uint32_t mine = s > c_at ? s - c_at : 0u;
   const uint32_t spp = (uint32_t)V.S.cam.spp;
   return total + mine < spp ? spp - total - mine : 0u;
 }
 
-// Ask (one writer lane): enqueue the request and point the cursor at the successor to come.
-RT_D void recut_request(const Book1View &V, uint32_t pix, uint32_t seg, uint32_t x, uint32_t s, bool wave, bool writer,
-                        uint32_t &tc, uint32_t &st) {
+// Chain k of pixel pix, at stream offset x with s samples (segment 0) / records (k >= 1) taken, in the
+// launch's tail: ask for a cut if much of its stream is left (one writer lane enqueues).  The cut point
+// is a fraction of the draws left before k's successor (a last segment: of the pixel's remaining true
+// samples times k's draws per sample) ahead of x.  Sets kWatch (asked) or kNoAsk (too little left).
+RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, bool writer, uint32_t &tc) {
+  if (tc & (kWatch | kNoAsk) || (k & kItemUnsplit)) return;
+  const ChainPx P = V.ch_px[pix];
+  const uint32_t x0 = seg_start(V, P, k);
+  if (s < 4u || x <= x0) return;
+  const float per = (float)(x - x0) / (float)s;  // k's draws per sample
+  const uint32_t n = seg_next(V, P, k);
+  float draws;  // the draws k still has to run
+  if (n != kNone) {
+    const uint32_t sn = seg_start(V, P, n);
+    draws = sn > x ? (float)(sn - x) : 0.0f;
+  } else {
+    const uint32_t left = recut_left(V, P, k, s);
+    if (left == kLeftUnknown) return;  // (asks again later)
+    draws = (float)left * per;
+  }
+  const float samples = draws / per;
+  if (samples < (float)V.recut_min) {
+    tc |= kNoAsk;  // (what is left only shrinks)
+    return;
+  }
+  const uint32_t dx = ((uint32_t)(V.recut_frac * draws) + 1u) & ~1u;
+  const uint32_t x_new = x + (dx > 2u ? dx : 2u);
+  if (x_new >= 0x3fffffffu) return;
   if (writer) {
     const uint32_t idx = at_add(&V.mig[kMigRqPush], 1u);
     if (idx < V.rq_cap) {
       RecutReq &r = V.rq[idx];
-      r.pix = pix, r.seg = seg, r.x = x, r.s = s, r.wave = wave ? 1u : 0u;
+      r.pix = pix, r.seg = k, r.x_new = x_new, r.next = n;
+      const float mine = (1.0f - V.recut_frac) * samples;  // the new segment's share, x 2 + slack
+      const float cap = fminf(2.0f * mine + (float)V.recut_slack, (float)V.S.cam.spp + (float)V.recut_slack);
+      r.cap = (uint32_t)cap;
       __hip_atomic_store(&r.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  tc = (seg + 1u) << 24;  // (a request the helpers never act on leaves the chain as it was: no successor)
-  st = kStUnknown;
+  tc |= kWatch;
 }
 
-// Publish a cut for request r (wave-uniform: every lane calls; lane 0 decides and stores, the wave
-// fills the new record list).  Returns the new segment t >= 1 to run, or 0 when the request is stale
-// (the chain is no longer the last, has ended, the links before it are undecided) or not worth it.
+// Publish the cut a request asks for (one thread).  Returns the new segment t >= 1, or 0 when the
+// request is stale (k has ended, or was cut already), the pixel has no dynamic slot left or records
+// run out.  Order: the new slot's words, then k's successor word, then the count (release each).
 RT_D uint32_t recut_publish(const Book1View &V, const RecutReq &r) {
-  const bool l0 = wv_lane() == 0u;
   const ChainPx P = V.ch_px[r.pix];
   uint32_t *kdp = (uint32_t *)&V.ch_px[r.pix].kd;
-  uint32_t t = 0u, x_new = 0u, kd = 0u, base = 0u;
-  if (l0) {
-    kd = ld_acq(kdp);
-    const uint32_t tn = P.K + (kd & 0xffu);
-    const bool last = !(kd & 0x100u) && r.seg + 1u == tn && tn < P.K + kDynMax && tn < (uint32_t)kMaxSeg && r.s > 0u;
-    const uint64_t w = last ? ld_rel64(&V.ch_seg[P.end0 + r.seg]) : kEndEnded;
-    const uint32_t left = (w & kEndEnded) ? 0u : recut_left(V, P, r.seg, r.s);
-    if (left > 0u) {
-      const float per = (float)(r.x - seg_start(V, P, r.seg)) / (float)r.s;  // its draws per sample
-      const float ahead = V.recut_frac[r.wave ? 1 : 0] * (float)left * per;
-      const uint32_t dx = ((uint32_t)fminf(ahead, 1e9f) + 1u) & ~1u;
-      x_new = r.x + (dx > 2u ? dx : 2u);
-      if (left >= V.recut_min && x_new > r.x && x_new < 0x3fffffffu && at_cas(kdp, kd, kd | 0x100u)) {  // lock
-        const unsigned long long b =
-            __hip_atomic_fetch_add(V.rec_count, (unsigned long long)V.cap_dyn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (b + V.cap_dyn <= V.rec_cap && b + V.cap_dyn <= 0xffffffffull) {
-          t = tn;
-          base = (uint32_t)b;
-        } else {
-          st_rel(kdp, kd);  // out of records: unlock, no cut
-        }
+  const uint32_t kd = ld_acq(kdp);
+  const uint32_t t = P.K + (kd & 0xffu);
+  uint32_t ok = 0u;
+  if (!(kd & 0x100u) && t < P.K + kDynMax && t < (uint32_t)kMaxSeg &&
+      !(ld_rel64(&V.ch_seg[P.end0 + r.seg]) & kEndEnded) && seg_next(V, P, r.seg) == r.next &&
+      at_cas(kdp, kd, kd | 0x100u)) {  // lock the pixel's slots
+    const unsigned long long b =
+        __hip_atomic_fetch_add(V.rec_count, (unsigned long long)r.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (b + r.cap <= (unsigned long long)ld_rel(V.rec_filled)) {
+      SegDyn &d = V.ch_sd[P.end0 + t];
+      st_rel(&d.start, r.x_new);
+      st_rel(&d.base, (uint32_t)b);
+      st_rel(&d.cap, r.cap);
+      st_rel(&d.next, r.next + 1u);  // (kNone + 1: none)
+      st_rel64(&V.ch_seg[P.end0 + t], 0ull);
+      __hip_atomic_store(&V.ch_sd[P.end0 + r.seg].next, t + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      ok = t;
+    }
+    __hip_atomic_store(kdp, (kd & 0xffu) + (ok ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // unlock
+  }
+  if (V.recut_stats) at_add(&V.recut_stats[ok ? 0 : 1], 1u);
+  return ok;
+}
+
+// Take the next request (one thread): its index, or -1 when the queue is empty.
+RT_D int recut_pop(const Book1View &V) {
+  for (int tries = 0; tries < 4; tries++) {
+    const uint32_t p = ld_rel(&V.mig[kMigRqPop]);
+    uint32_t q = ld_rel(&V.mig[kMigRqPush]);
+    q = q < V.rq_cap ? q : V.rq_cap;
+    if (p >= q) return -1;
+    if (at_cas(&V.mig[kMigRqPop], p, p + 1u)) {
+      const RecutReq *rp = &V.rq[p];
+      while (__hip_atomic_load(&rp->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != V.mig_epoch) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_s_sleep(1);
+#endif
       }
+      return (int)p;
     }
   }
-  t = wv_first(t);
-  if (t == 0u) return 0u;
-  base = wv_first(base);
-  for (uint32_t q = wv_lane(); q < V.cap_dyn; q += wv_width()) st_rel(&V.ch_end[base + q], kRecFill);
-  wv_fence_release();  // (every lane: its fills before the words that publish them)
-  if (l0) {
-    st_rel64(&V.ch_seg[P.end0 + t], 0ull);
-    st_rel64(&V.ch_dyn[P.end0 + t], ((uint64_t)base << 32) | x_new);
-    __hip_atomic_store(kdp, (kd & 0xffu) + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // publish t
-  }
-  return t;
+  return -1;
 }
 
 // ---------------------------------------------------------------- whole-wave work items
@@ -857,8 +893,8 @@ RT_D uint32_t recut_publish(const Book1View &V, const RecutReq &r) {
 // values and runs the same shading), and each ray is traced by the wave (bf_candidate + bf_verify,
 // or the exact scan).  The item is a whole pixel (kMode 0: its samples in order), or a chain
 // (kMode 2: segment / unsplit pixel, with the same boundary protocol as a lane).
-// tail: the launch's tail is known to have begun (a helper runs this item): a last segment asks for a
-// cut at once; otherwise it checks the helper count every ~20 us.
+// tail: the launch's work items are all handed out (a helper runs this item): the chain may ask for a
+// cut (recut_ask); whole-wave items at the launch's start never do.
 template <int kMode>
 RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix, uint32_t seg,
                            uint8_t *__restrict__ out, const MigRec *res = nullptr, bool tail = false) {
@@ -882,7 +918,6 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
   } else if (kMode == 2 && !(seg & kItemUnsplit)) {
     chain_start(V, (uint32_t)pix, seg, g, tc, st);
   }
-  uint64_t gate_next = 0;
   const bool use_bf = V.n_bf_leaves > 0;
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
   if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
@@ -892,14 +927,9 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
       if (__builtin_amdgcn_readfirstlane((int)done)) break;
-      if (V.rq && recut_candidate(seg, tc)) {  // a last segment in the launch's tail: ask for a cut
-        if (!tail && wall_clock64() >= gate_next) {
-          tail = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.recut_idle;
-          tail = __builtin_amdgcn_readfirstlane((int)tail);
-          gate_next = wall_clock64() + 2000u;
-        }
-        if (tail && recut_left(V, V.ch_px[pix], seg, s) >= V.recut_min)
-          recut_request(V, (uint32_t)pix, seg, g.n, s, true, lane0, tc, st);
+      if (V.rq && tail && (s & 3u) == 0u) {  // the launch's tail: a long chain asks for a cut
+        recut_ask(V, (uint32_t)pix, seg, g.n, s, lane0, tc);
+        tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
       }
     } else if (s == (uint32_t)cam.spp) {
       break;
@@ -1058,9 +1088,9 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
       if (V.mig_drop && l0) drop = atomicAdd(&V.mig[kMigDropped], 1u) < V.mig_drop;
       if (!__builtin_amdgcn_readfirstlane(drop)) {
         __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
-        render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
+        render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r, V.rq != nullptr);
         __builtin_amdgcn_s_setprio(0);
-        if (l0) mig_item_done(V, total_own);
+        if (l0 && !seg_dynamic(V, r.pix, r.seg)) mig_item_done(V, total_own);  // (a cut is no item of the launch)
       }
       if (l0) atomicAdd(box + kMigCredits, 1u);
       idle_since = wall_clock64();
@@ -1071,34 +1101,31 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
     // queues an item to it while it runs a segment), and gives it again afterwards.
     if (V.rq) {
       int req = -1;
-      if (l0) {
-        const uint32_t p = ld_rel(&V.mig[kMigRqPop]);
-        uint32_t q = ld_rel(&V.mig[kMigRqPush]);
-        q = q < V.rq_cap ? q : V.rq_cap;
-        if (p < q) {
-          uint32_t c = ld_rel(box + kMigCredits);
-          bool mine = false;
-          while ((int32_t)c > 0 && !mine) {
-            const uint32_t prev = atomicCAS(box + kMigCredits, c, c - 1u);
-            mine = prev == c;
-            c = prev;
-          }
-          if (mine) {
-            if (atomicCAS(&V.mig[kMigRqPop], p, p + 1u) == p) req = (int)p;
-            else atomicAdd(box + kMigCredits, 1u);
-          }
+      if (l0 && ld_rel(&V.mig[kMigRqPop]) < ld_rel(&V.mig[kMigRqPush])) {
+        uint32_t c = ld_rel(box + kMigCredits);
+        bool mine = false;
+        while ((int32_t)c > 0 && !mine) {
+          const uint32_t prev = atomicCAS(box + kMigCredits, c, c - 1u);
+          mine = prev == c;
+          c = prev;
+        }
+        if (mine) {
+          req = recut_pop(V);
+          if (req < 0) atomicAdd(box + kMigCredits, 1u);
         }
       }
       req = __builtin_amdgcn_readfirstlane(req);
       if (req >= 0) {
-        const RecutReq *rp = &V.rq[(uint32_t)req];
-        while (__hip_atomic_load(&rp->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != V.mig_epoch)
-          __builtin_amdgcn_s_sleep(1);
-        const RecutReq r = *rp;
-        const uint32_t t = recut_publish(V, r);
+        uint32_t t = 0u, pix = 0u;
+        if (l0) {
+          const RecutReq r = V.rq[(uint32_t)req];
+          t = recut_publish(V, r);
+          pix = r.pix;
+        }
+        t = wv_first(t);
         if (t) {
           __builtin_amdgcn_s_setprio(2);
-          render_item_coop<kMode>(V, items9, (int64_t)wv_first(r.pix), t, out, nullptr, true);
+          render_item_coop<kMode>(V, items9, (int64_t)wv_first(pix), t, out, nullptr, true);
           __builtin_amdgcn_s_setprio(0);
         }
         if (l0) atomicAdd(box + kMigCredits, 1u);
@@ -1233,8 +1260,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
   uint64_t mig_next = 0;
-  bool recut_ok = false;   // re-cut gate (wave-uniform), likewise
-  uint64_t recut_next = 0;
+  bool work_gone = false;  // (wave-uniform) a lane of this wave found no work item left: the launch's tail
+  bool dyn = false;        // this lane runs a cut (a dynamic segment), not one of the launch's items
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
   int32_t pix = 0;  // (< 2^31: host-checked)
@@ -1311,16 +1338,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       }
       mig_try = mig_ok;
     }
-    // run-time re-cut: once more than recut_idle waves have become helpers, a last segment asks for a
-    // cut (RecutReq); the same rare read of the helper count, only by waves holding such a chain
-    if (kMode == 2 && V.rq && !recut_ok && __ballot(recut_candidate(seg, tc)) != 0) {
-      const uint64_t now = wall_clock64();
-      if (now >= recut_next) {
-        recut_ok = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.recut_idle;
-        recut_ok = __builtin_amdgcn_readfirstlane((int)recut_ok);
-        recut_next = now + 2000u;
-      }
-    }
     // ---------------- shading pass (Camera_ray_color body after hit(), src/raytracing.c:44-75)
     bool need_pixel = !have_result, need_sample = false;
     if (have_result) {
@@ -1377,7 +1394,18 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
         base = __shfl(base, first);
         const int64_t item = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
-        if (item >= total_own) {
+        work_gone = work_gone || __ballot(item >= total_own) != 0;
+        // no item left: run a cut a long chain asked for (RecutReq), if any; else this lane is done
+        uint32_t cut = 0u, cut_pix = 0u;
+        if (kMode == 2 && item >= total_own && V.rq) {
+          const int req = recut_pop(V);
+          if (req >= 0) {
+            const RecutReq r = V.rq[(uint32_t)req];
+            cut = recut_publish(V, r);
+            cut_pix = r.pix;
+          }
+        }
+        if (item >= total_own && cut == 0u) {
           mode = kExit;
           break;
         }
@@ -1385,12 +1413,16 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         s = 0;
         seg = kItemUnsplit;
         tc = kNoTarget;
+        dyn = cut != 0u;
         if (kMode == 2 && cont) {  // the true chain on from an exact position (chain_fold_kernel)
           const ChainCont c = V.ch_cont[item];
           pix = (int32_t)c.pix;
           s = (int)c.s;
           acc = mk(c.acc[0], c.acc[1], c.acc[2]);
           st = c.o;  // (applied below, after the seed)
+        } else if (kMode == 2 && dyn) {
+          pix = (int32_t)cut_pix;
+          seg = cut;
         } else if (kMode == 2) {
           const uint2 it = V.ch_items[item + work_offset];
           pix = (int32_t)it.x;
@@ -1413,13 +1445,12 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }
       if (kMode == 2 && chain_boundary(V, pix, seg, g.n, (uint32_t)s, acc, tc, st, out, true)) {
-        if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
+        if (kMode == kMigMode && V.mig_live > 0 && !dyn) mig_item_done(V, total_own);
         need_pixel = true;  // this item is finished
         continue;
       }
-      if (kMode == 2 && recut_ok && (s & 3) == 0 && recut_candidate(seg, tc) &&
-          recut_left(V, V.ch_px[pix], seg, (uint32_t)s) >= V.recut_min)
-        recut_request(V, (uint32_t)pix, seg, g.n, (uint32_t)s, false, true, tc, st);
+      if (kMode == 2 && V.rq && work_gone && (s & 3) == 0)  // the launch's tail: a long chain asks for a cut
+        recut_ask(V, (uint32_t)pix, seg, g.n, (uint32_t)s, true, tc);
       if (mig_try && !need_pixel && mig_push(V, (uint32_t)glane % kMigBoxes, pix, seg, (uint32_t)s, acc, g, tc, st)) {
         mode = kExit;  // handed over at this sample boundary
         need_sample = false;

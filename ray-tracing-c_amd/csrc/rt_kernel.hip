@@ -372,7 +372,7 @@ __global__ __launch_bounds__(1024) void lpt_coop_sort_kernel(const uint32_t *cos
 //   chain_wave_sort_kernel, chain_fill_kernel.
 // Counters (u32, ch_cnt): see kCn* below; [256, 512) lane bucket counts, [512, 768) their offsets.
 enum : int {
-  kCnItems = 0, kCnSplit = 1, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
+  kCnItems = 0, kCnSplit = 1, kCnFilled = 2, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
   kCnCoopWaves = 7, kCnCoopCounter = 8, kCnNCoop = 9, kCnWaveWork = 10 /* u64 */, kCnCstar = 12, kCnCstarW = 13,
   kCnHist = 256, kCnOff = 512, kCnCstarTab = 768, kCnWords = 1024
 };
@@ -417,7 +417,7 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
                                                          uint32_t *cnt, ChainModel m, b1::ChainPx *px,
-                                                         uint64_t *seg, uint32_t *kk, uint32_t *split) {
+                                                         uint64_t *seg, b1::SegDyn *sd, uint32_t *kk, uint32_t *split) {
   __shared__ uint32_t h[256];
   __shared__ unsigned long long wwork;
   for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
         P.cap_last = cap_last;
         P.kd = 0u;
         px[p] = P;
-        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull;
+        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull, sd[e0 + k].next = 0u;  // (planned successors)
         split[atomicAdd(&cnt[kCnSplit], 1u)] = (uint32_t)p;
       }
     }
@@ -565,9 +565,13 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
   for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = make_uint2((uint32_t)(val[i] >> 32), (uint32_t)val[i]);
 }
 
-__global__ void chain_fill_kernel(const uint32_t *cnt, uint32_t *ch_end, uint32_t cap) {
-  const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
+// ch_end = kRecFill for the planned records and a reserve behind them, from which run-time cuts
+// (rt_book1.h: recut_publish) allocate their record lists; cnt[kCnFilled] = the end of the filled range.
+constexpr unsigned long long kRecutReserve = 16u << 20;  // records (64 MB of end words)
+__global__ void chain_fill_kernel(uint32_t *cnt, uint32_t *ch_end, uint32_t cap) {
+  const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec] + kRecutReserve;
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kCnFilled] = n;
   const uint32_t n4 = n / 4;
   uint4 *e4 = (uint4 *)ch_end;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x)
@@ -635,10 +639,9 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
-  bool recut = true;  // run-time re-cut of last segments (rt_book1.h: RecutReq)
-  int recut_idle = 25;     //   once this percentage of the grid's waves has become helpers
-  int recut_min = 32;      //   for chains with at least this many true samples left
-  float recut_frac_lane = 0.3f, recut_frac_wave = 0.5f;  //   the new segment starts this share of them ahead
+  bool recut = true;       // run-time re-cuts in a launch's tail (rt_book1.h: RecutReq)
+  int recut_min = 32;      //   of chains with at least this many samples left
+  float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
   int lane_occ = 5;   // lane kernel occupancy target
   int sample_cost = 0;     // cost pre-pass: per-sample latency in traversal steps (measured: 75-250 slower; off)
@@ -658,10 +661,10 @@ struct Config {
     if (c.mig_wait_us < 0) c.mig_wait_us = 0;
     c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
     c.recut = env_flag("RT_RECUT", c.recut);
-    c.recut_idle = env_int("RT_RECUT_IDLE", c.recut_idle);
     c.recut_min = env_int("RT_RECUT_MIN", c.recut_min);
-    if (c.recut_min < 2) c.recut_min = 2;
-    if (const char *e = getenv("RT_RECUT_FRAC")) sscanf(e, "%f,%f", &c.recut_frac_lane, &c.recut_frac_wave);
+    if (c.recut_min < 4) c.recut_min = 4;
+    c.recut_frac = env_float("RT_RECUT_FRAC", c.recut_frac);
+    c.recut_frac = c.recut_frac < 0.05f ? 0.05f : (c.recut_frac > 0.95f ? 0.95f : c.recut_frac);
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
@@ -760,7 +763,7 @@ struct rt_device_scene {
   float4 *ch_acc0 = nullptr;
   b1::ChainCont *ch_cont = nullptr;
   uint32_t ch_seg_cap = 0;
-  uint64_t *ch_dyn = nullptr;       // dynamic segments' start / record base (run-time re-cut)
+  b1::SegDyn *ch_sd = nullptr;      // per segment slot: dynamic segments, successor words (run-time re-cut)
   b1::RecutReq *rq = nullptr;       // re-cut request queue
   uint32_t rq_cap = 0;
   void *ch_rec_arena = nullptr;
@@ -1180,7 +1183,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     const size_t cs[11] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
                            npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
                            nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont),
-                           nseg * sizeof(uint64_t), (size_t)d->rq_cap * sizeof(b1::RecutReq)};
+                           nseg * sizeof(b1::SegDyn), (size_t)d->rq_cap * sizeof(b1::RecutReq)};
     size_t co[11], ct = 0;
     for (int k = 0; k < 11; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
     HIP_OK(hipMalloc(&d->ch_arena, ct));
@@ -1194,7 +1197,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_wave_key = (uint64_t *)(c + co[6]);
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
-    d->ch_dyn = (uint64_t *)(c + co[9]);
+    d->ch_sd = (b1::SegDyn *)(c + co[9]);
     d->rq = (b1::RecutReq *)(c + co[10]);
     if (cfg.px_time) {
       HIP_OK(hipMalloc(&d->seg_time, nseg * 2 * sizeof(uint32_t)));
@@ -1498,7 +1501,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   uint32_t *end = (uint32_t *)(col + d->ch_rec_cap);
   hipLaunchKernelGGL(chain_params_kernel, dim3(1), dim3(64), 0, st, sums, d->ch_cnt, m);
   hipLaunchKernelGGL(chain_plan_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, d->draw_out, n, d->ch_cnt, m, d->ch_px,
-                     d->ch_seg, d->ch_k, d->ch_split);
+                     d->ch_seg, d->ch_sd, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
                      d->ch_wave_key);
@@ -1533,17 +1536,16 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
-  V.ch_dyn = d->ch_dyn;
+  V.ch_sd = d->ch_sd;
   V.rec_count = (unsigned long long *)(d->ch_cnt + kCnRec);
-  V.rec_cap = d->ch_rec_cap;
-  V.cap_dyn = (uint32_t)V.S.cam.spp + (uint32_t)cfg.chain_slack;
-  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // (helpers run the cuts: they need migration + the LDS scene)
+  V.rec_filled = d->ch_cnt + kCnFilled;
+  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // (helpers run cuts too: migration + the LDS scene)
     V.rq = d->rq;
     V.rq_cap = d->rq_cap;
-    V.recut_idle = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.recut_idle / 100);
     V.recut_min = (uint32_t)cfg.recut_min;
-    V.recut_frac[0] = cfg.recut_frac_lane;
-    V.recut_frac[1] = cfg.recut_frac_wave;
+    V.recut_frac = cfg.recut_frac;
+    V.recut_slack = (uint32_t)cfg.chain_slack;
+    V.recut_stats = d->status + 4;
   }
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
@@ -1568,8 +1570,11 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
         pushed += bx[b1::kMigPush] < V.mig_cap / b1::kMigBoxes ? bx[b1::kMigPush] : V.mig_cap / b1::kMigBoxes;
         popped += bx[b1::kMigPop];
       }
-      fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u\n", mw[b1::kMigHelpers],
-              (unsigned long long)pushed, (unsigned long long)popped, mw[b1::kMigDone]);
+      uint32_t rs[2] = {0u, 0u};
+      HIP_OK(hipMemcpy(rs, d->status + 4, sizeof rs, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u; re-cut requests %u "
+              "popped %u, cuts %u declined %u (scene totals)\n", mw[b1::kMigHelpers], (unsigned long long)pushed,
+              (unsigned long long)popped, mw[b1::kMigDone], mw[b1::kMigRqPush], mw[b1::kMigRqPop], rs[0], rs[1]);
     }
   }
   hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 4 + 1 < 2048 ? npix / 4 + 1 : 2048)), dim3(256), 0, st,
@@ -2066,7 +2071,25 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
       r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len;
     }
   }
-  return (int64_t)n_items;
+  // then the dynamic segments (run-time re-cuts, run by helper waves): whole-wave flag 2
+  size_t k = n_items;
+  std::vector<uint32_t> split(c[kCnSplit]);
+  HIP_OK(hipMemcpy(split.data(), d->ch_split, split.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t p : split) {
+    const b1::ChainPx &P = px[p];
+    for (uint32_t t = P.K; t < P.K + (P.kd & 0xffu) && P.end0 + t < n_seg; t++, k++) {
+      if ((int64_t)k >= max_rows) continue;
+      const uint64_t w = seg[P.end0 + t];
+      uint32_t *r = rows + 16 * k;
+      memset(r, 0, 16 * sizeof(uint32_t));
+      r[0] = p, r[1] = t, r[2] = P.K, r[3] = 2u;
+      r[4] = sgt[2 * (P.end0 + t)], r[5] = sgt[2 * (P.end0 + t) + 1];
+      r[6] = b1::end_n(w);
+      r[7] = ((w & b1::kEndEnded) && !(w & b1::kEndNoLink) ? 1u : 0u) | ((w & b1::kEndEnded) ? 2u : 0u);
+      r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len, r[11] = draws[p], r[12] = costs[p];
+    }
+  }
+  return (int64_t)k;
 }
 
 // Name of the frame kernel rt_render_rows_async launches for this scene over the whole image (as

@@ -38,7 +38,8 @@ end = (r[:, 5] - t0) / 1e5
 print(f"world={world} rank={rank} ms={t * 1e3:.1f} kernel_ms={ds.last_launch_ms():.1f} items={m} "
       f"last_end={end.max():.1f} ms", flush=True)
 kinds = {"unsplit lane": (r[:, 2] == 1) & (r[:, 3] == 0), "unsplit wave": (r[:, 2] == 1) & (r[:, 3] == 1),
-         "segment lane": (r[:, 2] > 1) & (r[:, 3] == 0), "segment wave": (r[:, 2] > 1) & (r[:, 3] == 1)}
+         "segment lane": (r[:, 2] > 1) & (r[:, 3] == 0), "segment wave": (r[:, 2] > 1) & (r[:, 3] == 1),
+         "re-cut (dyn)": r[:, 3] == 2}
 for name, k in kinds.items():
     if k.any():
         d = end[k] - start[k]
@@ -46,7 +47,7 @@ for name, k in kinds.items():
               f"  start max {start[k].max():.1f}  duration p50/p99/max {np.percentile(d, [50, 99, 100]).round(1)}"
               f"  records p50/max {np.percentile(r[k, 6], [50, 100])}", flush=True)
 # coupling: per split pixel, samples computed (head samples + every record) against spp
-sp = r[:, 2] > 1
+sp = (r[:, 2] > 1) & (r[:, 3] < 2)  # planned segments
 if sp.any():
     pix = r[sp, 0]
     tot = np.bincount(pix, weights=r[sp, 6])
@@ -67,7 +68,7 @@ if sp.any():
     print(f"  planned stream (seg_len*K) / (pre-pass draws * spp/8) p50 {np.median(est / np.maximum(1, r[sp, 11] * spp / 8)):.2f}", flush=True)
 # items in flight over time (lanes: 64 per wave of the grid); whole-wave items count 64
 ts = np.arange(0.0, end.max() + 5.0, 5.0)
-w = np.where(r[:, 3] == 1, 64, 1)
+w = np.where(r[:, 3] >= 1, 64, 1)
 inflight = [int(w[(start <= t) & (end > t)].sum()) for t in ts]
 print("  lane-equivalents in flight every 5 ms: " + " ".join(f"{t:.0f}:{v // 1000}k" for t, v in zip(ts, inflight)), flush=True)
 last = np.argsort(-end)[:16]

@@ -137,8 +137,9 @@ int main(int argc, char **argv) {
   const size_t rec_room = rec + (recut ? (size_t)split.size() * b1::kDynMax * cap_dyn / 4 : 0);  // (cuts may run out: fine)
   col.assign(rec_room, make_float4(0, 0, 0, 0));
   endw.assign(rec_room, b1::kRecFill);
-  std::vector<uint64_t> dyn(seg.size(), 0ull);
+  std::vector<b1::SegDyn> sd(seg.size(), b1::SegDyn{0u, 0u, 0u, 0u});
   std::vector<uint32_t> mig(b1::kMigWords, 0u);
+  const uint32_t filled = (uint32_t)rec_room;
   std::vector<b1::RecutReq> rq(4 * split.size() + 16);
   unsigned long long rec_count = rec;
   b1::Book1View V;
@@ -149,13 +150,13 @@ int main(int argc, char **argv) {
   V.ch_col = col.data();
   V.ch_end = endw.data();
   V.ch_acc0 = acc0.data();
-  V.ch_dyn = dyn.data();
+  V.ch_sd = sd.data();
   V.mig = mig.data();
   V.mig_epoch = 1u;
-  V.cap_dyn = cap_dyn;
   V.rec_count = &rec_count;
-  V.rec_cap = rec_room;
-  V.recut_min = 2u;
+  V.rec_filled = &filled;
+  V.recut_min = 4u;
+  V.recut_slack = slack;
   if (recut) {
     V.rq = rq.data();
     V.rq_cap = (uint32_t)rq.size();
@@ -179,15 +180,17 @@ int main(int argc, char **argv) {
       live.pop_back();
       continue;
     }
-    // a last segment asks for a cut (the kernels: in the launch's tail); a helper publishes one
-    if (V.rq && (rnd() & 7u) == 0u && b1::recut_candidate(c.seg, c.tc) &&
-        b1::recut_left(V, px[c.pix], c.seg, c.s) >= V.recut_min) {
-      b1::recut_request(V, (uint32_t)c.pix, c.seg, c.g.n, c.s, c.wave, true, c.tc, c.st);
-      requests++;
+    // a chain asks for a cut (the kernels: in the launch's tail) at a random point of its remaining
+    // draws; a server publishes requests at random times
+    if (V.rq && (rnd() & 7u) == 0u && (c.s & 3u) == 0u) {
+      V.recut_frac = 0.02f + 0.96f * (float)(rnd() % 1000u) / 1000.0f;
+      const uint32_t before = mig[b1::kMigRqPush];
+      b1::recut_ask(V, (uint32_t)c.pix, c.seg, c.g.n, c.s, true, c.tc);
+      requests += mig[b1::kMigRqPush] - before;
     }
-    if (V.rq && (rnd() & 3u) == 0u && mig[b1::kMigRqPop] < mig[b1::kMigRqPush] && mig[b1::kMigRqPop] < V.rq_cap) {
-      const b1::RecutReq r = rq[mig[b1::kMigRqPop]++];
-      V.recut_frac[0] = V.recut_frac[1] = 0.02f + 0.96f * (float)(rnd() % 1000u) / 1000.0f;  // any cut point
+    int req = -1;
+    if (V.rq && (rnd() & 3u) == 0u && (req = b1::recut_pop(V)) >= 0) {
+      const b1::RecutReq r = rq[(uint32_t)req];
       const uint32_t t = b1::recut_publish(V, r);
       if (t) {
         cuts++;
@@ -228,7 +231,7 @@ int main(int argc, char **argv) {
     uint32_t total = b1::end_n(w), t = b1::end_t(w), c = b1::end_c(w);
     uint32_t o = c == 0 ? b1::seg_start(V, P, t) : endw[b1::rec_index(V, P, t, c - 1)];
     for (;;) {
-      if (t == 0 || t >= P.K + (P.kd & 0xffu)) {
+      if (t == 0 || t >= P.K + b1::kDynMax) {
         fprintf(stderr, "pixel %u: bad link %u\n", p, t);
         return 3;
       }
