@@ -808,17 +808,28 @@ RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, ui
   const float per = (float)(x - x0) / (float)s;  // k's draws per sample
   const uint32_t n = seg_next(V, P, k);
   float draws;  // the draws k still has to run
-  if (n != kNone) {
+  bool to_end = n == kNone;
+  if (!to_end) {
     const uint32_t sn = seg_start(V, P, n);
-    draws = sn > x ? (float)(sn - x) : 0.0f;
-  } else {
+    if (sn > x) {
+      draws = (float)(sn - x);
+    } else if ((float)(x - sn) < 16.0f * per) {
+      return;  // coupling into n normally takes a few samples past its start: ask later
+    } else {
+      // past n's start without coupling: n's chain may never meet this one (a parity trap: one odd
+      // draw count flips the true chain onto odd offsets, where an even-started segment never lands),
+      // so this chain may have to run to the pixel's end -- a cut at its own parity shares that out
+      to_end = true;
+    }
+  }
+  if (to_end) {
     const uint32_t left = recut_left(V, P, k, s);
     if (left == kLeftUnknown) return;  // (asks again later)
     draws = (float)left * per;
   }
   const float samples = draws / per;
   if (samples < (float)V.recut_min) {
-    tc |= kNoAsk;  // (what is left only shrinks)
+    if (!to_end || n == kNone) tc |= kNoAsk;  // (what is left only shrinks)
     return;
   }
   const uint32_t dx = ((uint32_t)(V.recut_frac * draws) + 1u) & ~1u;
@@ -829,9 +840,9 @@ RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, ui
     if (idx < V.rq_cap) {
       RecutReq &r = V.rq[idx];
       r.pix = pix, r.seg = k, r.x_new = x_new, r.next = n;
-      const float mine = (1.0f - V.recut_frac) * samples;  // the new segment's share, x 2 + slack
-      const float cap = fminf(2.0f * mine + (float)V.recut_slack, (float)V.S.cam.spp + (float)V.recut_slack);
-      r.cap = (uint32_t)cap;
+      // (as many records as a planned last segment: a list that fills ends its chain unlinked, and the
+      // pixel then needs a continuation launch)
+      r.cap = (uint32_t)V.S.cam.spp + V.recut_slack;
       __hip_atomic_store(&r.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
