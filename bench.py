@@ -172,7 +172,8 @@ def main():
         else:
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
-    sc = rtc.Scene.preset(args.scene, args.width, args.spp, args.depth)
+    # (scenes 3 and 7: the documented substitute earth picture, DESIGN.md §7 -- the reference repo ships none)
+    sc = rtc.Scene.preset(args.scene, args.width, args.spp, args.depth, substitute_earth=True)
     W, H, spp = sc.width, sc.height, sc.spp
     row0, stride, n_rows = rtc.rows_of(H, rank, world)
     ds = rtc.DeviceScene(sc, local)

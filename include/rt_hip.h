@@ -35,6 +35,11 @@ void rt_flat_free(rt_flat_scene *scene);
  * src/main.c:294-329), built by this library with the reference's defaults (src/main.c:278-287);
  * width <= 0 / spp <= 0 / max_depth <= 0 keep the default (500 / 100 / 50). */
 rt_flat_scene *rt_scene_preset(int scene_id, int width, int spp, int max_depth);
+/* The same, with relative image file names (scenes 3 and 7: "earthmap.jpg") looked up in image_dir
+ * instead of the working directory (NULL: the working directory).  An image that cannot be read
+ * (neither a baseline JPEG nor a binary PPM) makes both return NULL with rt_last_error() set; the
+ * reference's own Image_new aborts instead (src/texture.c:41), and so does this library's. */
+rt_flat_scene *rt_scene_preset_in(int scene_id, int width, int spp, int max_depth, const char *image_dir);
 
 /* ---- device side -------------------------------------------------------------------------- */
 int rt_device_count(void);

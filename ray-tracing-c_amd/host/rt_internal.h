@@ -47,4 +47,12 @@ const char *rt_build_scene(int scene_id, World *world, Camera *camera);
 /* error channel shared with the HIP side */
 void rt_set_error(const char *fmt, ...);
 
+/* baseline JPEG -> RGB (rt_jpeg.c); NULL on failure with the reason in err */
+RT_HIDDEN uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height, char *err, size_t err_len);
+/* Image_new failures: the reference aborts (src/texture.c:41); rt_scene_preset instead records the
+ * failure (rt_image_soft_begin/end) and returns NULL with the message in rt_last_error().  dir: where
+ * relative image file names are looked up (NULL: the working directory, as the reference does) */
+RT_HIDDEN void rt_image_soft_begin(const char *dir);
+RT_HIDDEN int rt_image_soft_end(void);  /* 0: every image loaded */
+
 #endif /* RT_INTERNAL_H */

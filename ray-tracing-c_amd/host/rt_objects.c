@@ -455,34 +455,75 @@ Texture *Checker_new(float scale, Texture *even, Texture *odd) {
   return &t->texture;
 }
 
-/* Binary PPM (P6, maxval 255) reader; returns NULL if the file is absent or not P6. */
-static uint8_t *read_ppm(const char *path, int *width, int *height) {
-  FILE *f = fopen(path, "rb");
-  if (!f) return NULL;
+/* Binary PPM (P6, maxval 255) from memory; NULL if it is not one. */
+static uint8_t *decode_ppm(const uint8_t *buf, size_t len, int *width, int *height) {
+  int w = 0, h = 0, maxval = 0, at = 0;
   char magic[3] = {0};
-  int w = 0, h = 0, maxval = 0;
-  uint8_t *px = NULL;
-  if (fscanf(f, "%2s %d %d %d", magic, &w, &h, &maxval) == 4 && strcmp(magic, "P6") == 0 && w > 0 && h > 0 &&
-      maxval == 255 && fgetc(f) != EOF) {
-    px = my_malloc((size_t)w * h * 3);
-    if (fread(px, 1, (size_t)w * h * 3, f) != (size_t)w * h * 3) {
-      free(px);
-      px = NULL;
-    }
-  }
-  fclose(f);
-  if (px) {
-    *width = w;
-    *height = h;
-  }
+  char head[64] = {0};
+  memcpy(head, buf, len < sizeof head - 1 ? len : sizeof head - 1);
+  if (sscanf(head, "%2s %d %d %d%n", magic, &w, &h, &maxval, &at) != 4 || strcmp(magic, "P6") != 0 || w <= 0 ||
+      h <= 0 || maxval != 255)
+    return NULL;
+  const size_t n = (size_t)w * h * 3, off = (size_t)at + 1;  /* one whitespace byte after maxval */
+  if (off + n > len) return NULL;
+  uint8_t *px = my_malloc(n);
+  memcpy(px, buf + off, n);
+  *width = w;
+  *height = h;
   return px;
 }
 
+static _Thread_local int g_image_soft = 0, g_image_failed = 0;
+static _Thread_local const char *g_image_dir = NULL;
+void rt_image_soft_begin(const char *dir) { g_image_soft = 1, g_image_failed = 0, g_image_dir = dir; }
+int rt_image_soft_end(void) {
+  g_image_soft = 0;
+  g_image_dir = NULL;
+  return g_image_failed;
+}
+
+/* Image_init (src/texture.c:38-42): the file's content decides the format -- baseline JPEG (as the
+ * reference's stb_image decodes it: rt_jpeg.c) or binary PPM (the documented substitute picture) */
 void Image_init(Image *self, char *filename) {
   self->texture.value = rt_tex_image_value;
-  self->buffer = read_ppm(filename, &self->width, &self->height);
-  if (self->buffer == NULL) {  /* the reference asserts here (src/texture.c:38-42) */
-    fprintf(stderr, "rt: Image_new(\"%s\"): Unable to read image (this library decodes binary PPM only)\n", filename);
+  self->buffer = NULL;
+  char why[160] = "cannot open the file";
+  char path[4096];
+  if (g_image_dir && filename[0] != '/' && snprintf(path, sizeof path, "%s/%s", g_image_dir, filename) < (int)sizeof path)
+    filename = path;
+  FILE *f = fopen(filename, "rb");
+  if (f) {
+    uint8_t *buf = NULL;
+    size_t len = 0, cap = 0;
+    for (;;) {
+      if (len == cap) {
+        cap = cap ? 2 * cap : 1 << 20;
+        buf = realloc(buf, cap);
+        if (!buf) break;
+      }
+      const size_t got = fread(buf + len, 1, cap - len, f);
+      len += got;
+      if (got == 0) break;
+    }
+    fclose(f);
+    if (buf && len >= 2 && buf[0] == 0xff && buf[1] == 0xd8) {
+      self->buffer = rt_jpeg_decode(buf, len, &self->width, &self->height, why, sizeof why);
+    } else if (buf) {
+      self->buffer = decode_ppm(buf, len, &self->width, &self->height);
+      snprintf(why, sizeof why, "neither a baseline JPEG nor a binary PPM");
+    }
+    free(buf);
+  }
+  if (self->buffer == NULL) {  /* the reference asserts here (src/texture.c:41) */
+    if (g_image_soft) {  /* (rt_scene_preset: reported, not fatal) */
+      rt_set_error("Image_new(\"%s\"): unable to read image: %s", filename, why);
+      g_image_failed = 1;
+      self->width = self->height = 1;
+      self->buffer = my_malloc(3);
+      memset(self->buffer, 0, 3);
+      return;
+    }
+    fprintf(stderr, "rt: Image_new(\"%s\"): Unable to read image: %s\n", filename, why);
     abort();
   }
 }

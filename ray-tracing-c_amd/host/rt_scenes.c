@@ -234,14 +234,20 @@ const char *rt_build_scene(int scene_id, World *world, Camera *camera) {
   }
 }
 
-rt_flat_scene *rt_scene_preset(int scene_id, int width, int spp, int max_depth) {
+rt_flat_scene *rt_scene_preset_in(int scene_id, int width, int spp, int max_depth, const char *image_dir) {
   World world = {0};
   Camera camera = {0};
   rt_camera_defaults(&camera);
   if (width > 0) camera.img_width = width;
   if (spp > 0) camera.samples_per_pixel = spp;
+  rt_image_soft_begin(image_dir);
   (void)rt_build_scene(scene_id, &world, &camera);
+  if (rt_image_soft_end()) return NULL; /* (rt_last_error() names the image) */
   if (max_depth > 0) camera.max_depth = max_depth;
   Camera_init(&camera);
   return rt_flatten(&camera, &world); /* the scene graph is leaked, as in the reference driver */
+}
+
+rt_flat_scene *rt_scene_preset(int scene_id, int width, int spp, int max_depth) {
+  return rt_scene_preset_in(scene_id, width, spp, max_depth, NULL);
 }

@@ -117,6 +117,8 @@ def lib() -> ctypes.CDLL:
         P = POINTER(RtFlatScene)
         L.rt_scene_preset.argtypes = [c_int, c_int, c_int, c_int]
         L.rt_scene_preset.restype = P
+        L.rt_scene_preset_in.argtypes = [c_int, c_int, c_int, c_int, c_char_p]
+        L.rt_scene_preset_in.restype = P
         L.rt_flat_free.argtypes = [P]
         L.rt_flat_free.restype = None
         L.rt_device_count.restype = c_int
@@ -165,21 +167,22 @@ class Scene:
         self._ptr = ptr
 
     @classmethod
-    def preset(cls, scene_id: int, width: int = 0, spp: int = 0, max_depth: int = 0) -> "Scene":
+    def preset(cls, scene_id: int, width: int = 0, spp: int = 0, max_depth: int = 0, image_dir: str | None = None,
+               substitute_earth: bool | None = None) -> "Scene":
         """Reference driver scene `scene_id` (0-7) with the reference defaults (500 px, 100 spp,
         depth 50) unless overridden; aspect ratio comes from the scene (src/main.c).
 
-        Scenes 3 and 7 read ``earthmap.jpg`` from the current directory, as the reference does; when
-        it is absent the preset is built in a directory holding the documented substitute picture
-        (rtc/earth.py) -- the explicit opt-in for tests and benches."""
-        if int(scene_id) in (3, 7) and not os.path.exists(earth.FILE_NAME):
-            cwd = os.getcwd()
-            os.chdir(substitute_dir())
-            try:
-                return cls(lib().rt_scene_preset(int(scene_id), int(width), int(spp), int(max_depth)))
-            finally:
-                os.chdir(cwd)
-        return cls(lib().rt_scene_preset(int(scene_id), int(width), int(spp), int(max_depth)))
+        Scenes 3 and 7 read ``earthmap.jpg`` (baseline JPEG or binary PPM) from `image_dir`, else
+        from the current directory, as the reference does.  The documented substitute picture
+        (rtc/earth.py) is used only on request: ``substitute_earth=True``, or the
+        environment variable ``RTC_SUBSTITUTE_EARTH=1`` (the test suite's and the benches' opt-in).
+        No process state (working directory) is changed."""
+        if substitute_earth is None:
+            substitute_earth = os.environ.get("RTC_SUBSTITUTE_EARTH", "0") == "1"
+        if image_dir is None and substitute_earth and int(scene_id) in (3, 7):
+            image_dir = substitute_dir()
+        d = image_dir.encode() if image_dir is not None else None
+        return cls(lib().rt_scene_preset_in(int(scene_id), int(width), int(spp), int(max_depth), d))
 
     @property
     def ptr(self):

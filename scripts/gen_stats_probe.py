@@ -17,7 +17,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     import rtc
 
     scene, width, spp = (int(x) for x in sys.argv[2:5])
-    sc = rtc.Scene.preset(scene, width, spp, 50)
+    sc = rtc.Scene.preset(scene, width, spp, 50, substitute_earth=True)
     t0 = time.perf_counter()
     rtc.render(sc, 1)
     print(f"frame_ms={1e3 * (time.perf_counter() - t0):.1f} {sc.width}x{sc.height}x{spp}", flush=True)

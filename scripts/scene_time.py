@@ -16,7 +16,7 @@ import rtc  # noqa: E402
 scene, width, spp = (int(x) for x in sys.argv[1:4])
 settings = sys.argv[4].split(";") if len(sys.argv) > 4 else [""]
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
-sc = rtc.Scene.preset(scene, width, spp, 50)
+sc = rtc.Scene.preset(scene, width, spp, 50, substitute_earth=True)
 st = torch.cuda.current_stream()
 buf = torch.empty((sc.height, sc.width, 3), dtype=torch.uint8, device="cuda")
 base = {k: os.environ.get(k) for s in settings for k in (kv.split("=")[0] for kv in s.split(",") if kv)}

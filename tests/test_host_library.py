@@ -184,3 +184,65 @@ def test_rows_partition_covers_frame_once():
                 row0, stride, n = rtc.rows_of(h, r, world)
                 rows += [row0 + k * stride for k in range(n)]
             assert sorted(rows) == list(range(h))
+
+
+def _flat_image(sc):
+    """The first image texture's RGB bytes of a flattened scene (rt_flat.h: rt_image)."""
+    s = sc.s
+    im = ctypes.cast(s.images, ctypes.POINTER(ctypes.c_int32 * 4))[0]
+    W, H = im[0], im[1]
+    return np.frombuffer(ctypes.string_at(s.image_bytes, W * H * 3), np.uint8).reshape(H, W, 3)
+
+
+@pytest.mark.parametrize("subsampling,mode,opts", [
+    ("4:4:4", "RGB", {}), ("4:2:0", "RGB", {}), ("4:2:2", "RGB", {}), ("4:4:4", "L", {}),
+    ("4:2:0", "RGB", {"optimize": True}), ("4:2:0", "RGB", {"restart_marker_rows": 1}),
+    ("4:4:4", "RGB", {"restart_marker_blocks": 5})])
+def test_image_new_decodes_baseline_jpeg(tmp_path, subsampling, mode, opts):
+    """Image_new on a real JPEG: the reference decodes earthmap.jpg with stb_image
+    (src/texture.c:38-42); host/rt_jpeg.c restates stb's baseline decoding (integer IDCT, triangle
+    chroma upsampling, fixed-point YCbCr).  stb is un-vendored here, so exact parity is unpinned; an
+    independent codec (Pillow's libjpeg) must agree within a few levels (different IDCT, upsampling
+    and colour rounding)."""
+    PIL = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(7)
+    h, w = 75, 131
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = np.stack([xx * 255 // (w - 1), yy * 255 // (h - 1), (xx ^ yy) & 255], -1)
+    img = (img + rng.integers(-20, 20, img.shape)).clip(0, 255).astype(np.uint8)
+    path = tmp_path / "earthmap.jpg"
+    try:
+        PIL.fromarray(img).convert(mode).save(path, quality=90, subsampling=subsampling, **opts)
+    except (TypeError, ValueError) as e:  # (an older Pillow without that option)
+        pytest.skip(f"Pillow cannot write this variant: {e}")
+    ref = np.asarray(PIL.open(path).convert("RGB")).astype(int)
+    got = _flat_image(rtc.Scene.preset(3, 40, 1, 1, image_dir=str(tmp_path))).astype(int)
+    assert got.shape == ref.shape
+    if subsampling == "4:2:2":  # (stb's h2v1 filter weights the last chroma sample's left neighbour 3:1)
+        got, ref = got[:, :-1], ref[:, :-1]
+    d = np.abs(got - ref)
+    assert d.max() <= 6 and d.mean() < 0.5, (d.max(), d.mean())
+
+
+def test_image_new_reports_unreadable_image(tmp_path):
+    """A progressive JPEG (not decoded) or a non-image file: the preset reports it (the reference and
+    this library's own Image_new abort, src/texture.c:41) instead of rendering a wrong texture."""
+    PIL = pytest.importorskip("PIL.Image")
+    PIL.fromarray(np.zeros((16, 16, 3), np.uint8)).save(tmp_path / "earthmap.jpg", progressive=True)
+    with pytest.raises(rtc.RtcError, match="progressive"):
+        rtc.Scene.preset(3, 40, 1, 1, image_dir=str(tmp_path))
+    (tmp_path / "earthmap.jpg").write_bytes(b"not an image")
+    with pytest.raises(rtc.RtcError, match="earthmap.jpg"):
+        rtc.Scene.preset(7, 40, 1, 1, image_dir=str(tmp_path))
+
+
+def test_preset_substitute_picture_is_opt_in(tmp_path, monkeypatch):
+    """the substitute earth picture is used only on request, and no working directory
+    is changed.  Without the opt-in and without earthmap.jpg, scene 7 is reported as unreadable."""
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RTC_SUBSTITUTE_EARTH", "0")
+    with pytest.raises(rtc.RtcError, match="earthmap.jpg"):
+        rtc.Scene.preset(7, 40, 1, 1)
+    sc = rtc.Scene.preset(7, 40, 1, 1, substitute_earth=True)
+    assert _flat_image(sc).shape == (512, 1024, 3)
+    assert os.getcwd() == str(tmp_path)
