@@ -207,6 +207,7 @@ struct Book1View {
   float recut_frac;      // the cut keeps this share of the chain's remaining draws on the chain
   uint32_t recut_slack;  // records of a dynamic segment: 2 x its share of samples + this
   uint32_t *recut_stats; // diagnostics (accumulated per scene): [0] cuts published, [1] requests declined
+  int32_t recut_lanes;   // chain launches: a lane cuts its chain for an idle lane of its own wave
 };
 
 // ---------------------------------------------------------------- chain segments (planned + dynamic)
@@ -797,14 +798,14 @@ RT_D uint32_t recut_left(const Book1View &V, const ChainPx &P, uint32_t k, uint3
 }
 
 // Chain k of pixel pix, at stream offset x with s samples (segment 0) / records (k >= 1) taken, in the
-// launch's tail: ask for a cut if much of its stream is left (one writer lane enqueues).  The cut point
-// is a fraction of the draws left before k's successor (a last segment: of the pixel's remaining true
-// samples times k's draws per sample) ahead of x.  Sets kWatch (asked) or kNoAsk (too little left).
-RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, bool writer, uint32_t &tc) {
-  if (tc & (kWatch | kNoAsk) || (k & kItemUnsplit)) return;
+// launch's tail: is a cut worth it?  The cut point is a fraction of the draws left before k's successor
+// (a last segment, or one stuck past its successor: of the pixel's remaining true samples times k's
+// draws per sample) ahead of x.  Fills r and returns true; sets kNoAsk when too little is left.
+RT_D bool recut_plan(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, uint32_t &tc, RecutReq &r) {
+  if (tc & (kWatch | kNoAsk) || (k & kItemUnsplit)) return false;
   const ChainPx P = V.ch_px[pix];
   const uint32_t x0 = seg_start(V, P, k);
-  if (s < 4u || x <= x0) return;
+  if (s < 4u || x <= x0) return false;
   const float per = (float)(x - x0) / (float)s;  // k's draws per sample
   const uint32_t n = seg_next(V, P, k);
   float draws;  // the draws k still has to run
@@ -814,7 +815,7 @@ RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, ui
     if (sn > x) {
       draws = (float)(sn - x);
     } else if ((float)(x - sn) < 16.0f * per) {
-      return;  // coupling into n normally takes a few samples past its start: ask later
+      return false;  // coupling into n normally takes a few samples past its start: ask later
     } else {
       // past n's start without coupling: n's chain may never meet this one (a parity trap: one odd
       // draw count flips the true chain onto odd offsets, where an even-started segment never lands),
@@ -824,26 +825,34 @@ RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, ui
   }
   if (to_end) {
     const uint32_t left = recut_left(V, P, k, s);
-    if (left == kLeftUnknown) return;  // (asks again later)
+    if (left == kLeftUnknown) return false;  // (asks again later)
     draws = (float)left * per;
   }
   const float samples = draws / per;
   if (samples < (float)V.recut_min) {
     if (!to_end || n == kNone) tc |= kNoAsk;  // (what is left only shrinks)
-    return;
+    return false;
   }
   const uint32_t dx = ((uint32_t)(V.recut_frac * draws) + 1u) & ~1u;
   const uint32_t x_new = x + (dx > 2u ? dx : 2u);
-  if (x_new >= 0x3fffffffu) return;
+  if (x_new >= 0x3fffffffu) return false;
+  r.pix = pix, r.seg = k, r.x_new = x_new, r.next = n;
+  // (as many records as a planned last segment: a list that fills ends its chain unlinked, and the
+  // pixel then needs a continuation launch)
+  r.cap = (uint32_t)V.S.cam.spp + V.recut_slack;
+  return true;
+}
+
+// Ask the helper waves (a chain a helper runs): enqueue the cut (one writer lane), watch the successor.
+RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, bool writer, uint32_t &tc) {
+  RecutReq r;
+  if (!recut_plan(V, pix, k, x, s, tc, r)) return;
   if (writer) {
     const uint32_t idx = at_add(&V.mig[kMigRqPush], 1u);
     if (idx < V.rq_cap) {
-      RecutReq &r = V.rq[idx];
-      r.pix = pix, r.seg = k, r.x_new = x_new, r.next = n;
-      // (as many records as a planned last segment: a list that fills ends its chain unlinked, and the
-      // pixel then needs a continuation launch)
-      r.cap = (uint32_t)V.S.cam.spp + V.recut_slack;
-      __hip_atomic_store(&r.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      RecutReq &q = V.rq[idx];
+      q.pix = r.pix, q.seg = r.seg, q.x_new = r.x_new, q.next = r.next, q.cap = r.cap;
+      __hip_atomic_store(&q.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   tc |= kWatch;
@@ -1218,7 +1227,11 @@ __device__ void render_wave_items(const Book1View &V, uint8_t *__restrict__ out,
   }
 }
 
-enum : int { kTrav = 0, kWait = 1, kExit = 2 };
+// kIdle: a chain-launch lane with no work item left; a lane of its wave may hand it a cut (below)
+enum : int { kTrav = 0, kWait = 1, kExit = 2, kIdle = 3 };
+// LDS behind the scene items (chain launches): per lane a handed-over cut {pixel, segment} (segment 0:
+// none), per wave the mask of idle lanes not yet handed one
+constexpr size_t kHandoffBytes = kBlock * sizeof(uint2) + kWaves * sizeof(unsigned long long);
 // traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
 // 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
 // schedule never changes a lane)
@@ -1271,8 +1284,19 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
   uint64_t mig_next = 0;
-  bool work_gone = false;  // (wave-uniform) a lane of this wave found no work item left: the launch's tail
   bool dyn = false;        // this lane runs a cut (a dynamic segment), not one of the launch's items
+  bool cut_ready = false;  // a cut was handed to this idle lane: its next item
+  // intra-wave cuts (chain launches): handoff slots and idle masks in LDS behind the scene items
+  uint2 *handoff = nullptr;
+  unsigned long long *idle_lds = nullptr;
+  const bool cuts = kMode == 2 && V.recut_lanes != 0 && !cont;
+  if (kMode == 2) {
+    char *hb = lds + (kLds ? (size_t)V.n_items9_alloc * 2 * sizeof(float4) : 0);
+    handoff = (uint2 *)hb;
+    idle_lds = (unsigned long long *)(hb + kBlock * sizeof(uint2));
+    handoff[tid] = make_uint2(0u, 0u);
+  }
+  const int wave_in_block = tid >> 6;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
   int32_t pix = 0;  // (< 2^31: host-checked)
@@ -1301,9 +1325,21 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
                                          : total - work_offset;
 
   for (;;) {
+    if (cuts && mode == kIdle) {  // a cut handed to this idle lane by a lane of its wave?
+      const uint2 h = handoff[tid];
+      if (h.y) {
+        handoff[tid].y = 0u;
+        pix = (int32_t)h.x;
+        seg = h.y;
+        cut_ready = true;
+        have_result = false;
+        mode = kWait;
+      }
+    }
     const uint64_t trav = __ballot(mode == kTrav);
     const uint64_t wait = __ballot(mode == kWait);
     if ((trav | wait) == 0) break;
+    const uint64_t idle = cuts ? __ballot(mode == kIdle) : 0ull;
     // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
@@ -1333,6 +1369,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       continue;
     }
     if (mode != kWait) continue;
+    if (cuts && idle && lane == __builtin_ctzll(wait)) idle_lds[wave_in_block] = idle;  // (this pass's idle lanes)
     // migration: the work items are gone (a lane of this wave found none) and few lanes are left
     // and enough of the GPU idles (more than mig_idle waves have become helpers): before that,
     // whole-wave traces would take issue slots from lanes that still make full use of them.  The
@@ -1398,6 +1435,21 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       }
     }
     while (need_pixel || need_sample) {
+      if (need_pixel && kMode == 2 && cut_ready) {  // a cut a lane of this wave handed over: run it
+        cut_ready = false;
+        dyn = true;
+        acc = mk(0.0f, 0.0f, 0.0f);
+        s = 0;
+        tc = kNoTarget;
+        {
+          const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
+          g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
+        }
+        chain_start(V, (uint32_t)pix, seg, g, tc, st);
+        need_pixel = false;
+        px_steps = 0;
+        if (V.px_time) chain_time(V, pix, seg, 0);
+      }
       if (need_pixel) {  // work stealing among the lanes that need an item right now
         const uint64_t want = __ballot(true);
         const int first = __builtin_ctzll(want);
@@ -1405,10 +1457,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
         base = __shfl(base, first);
         const int64_t item = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
-        work_gone = work_gone || __ballot(item >= total_own) != 0;
-        // no item left: run a cut a long chain asked for (RecutReq), if any; else this lane is done
+        // no item left: a whole-wave helper's queued cut, if any (RecutReq); else this lane is done --
+        // idle, where a lane of its wave may still hand it a cut of its own chain
         uint32_t cut = 0u, cut_pix = 0u;
-        if (kMode == 2 && item >= total_own && V.rq) {
+        if (kMode == 2 && item >= total_own && V.rq && !cuts) {
           const int req = recut_pop(V);
           if (req >= 0) {
             const RecutReq r = V.rq[(uint32_t)req];
@@ -1417,7 +1469,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           }
         }
         if (item >= total_own && cut == 0u) {
-          mode = kExit;
+          mode = cuts ? kIdle : kExit;
           break;
         }
         acc = mk(0.0f, 0.0f, 0.0f);
@@ -1460,8 +1512,31 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         need_pixel = true;  // this item is finished
         continue;
       }
-      if (kMode == 2 && V.rq && work_gone && (s & 3) == 0)  // the launch's tail: a long chain asks for a cut
-        recut_ask(V, (uint32_t)pix, seg, g.n, (uint32_t)s, true, tc);
+      // the launch's tail: this wave has idle lanes -- a long chain hands one of them a cut of itself
+      if (cuts && idle && (s & 3) == 0 && idle_lds[wave_in_block] != 0ull) {
+        RecutReq r;
+        if (recut_plan(V, (uint32_t)pix, seg, g.n, (uint32_t)s, tc, r)) {
+          unsigned long long m = idle_lds[wave_in_block], bit = 0ull;
+          while (m) {  // claim an idle lane (another lane of this wave may claim at the same time)
+            const unsigned long long b = m & (~m + 1ull);
+            const unsigned long long old = atomicAnd(&idle_lds[wave_in_block], ~b);
+            if (old & b) {
+              bit = b;
+              break;
+            }
+            m = old & ~b;
+          }
+          if (bit) {
+            const uint32_t t = recut_publish(V, r);
+            if (t) {
+              handoff[(wave_in_block << 6) + __builtin_ctzll(bit)] = make_uint2((uint32_t)pix, t);
+              tc |= kWatch;
+            } else {
+              atomicOr(&idle_lds[wave_in_block], bit);
+            }
+          }
+        }
+      }
       if (mig_try && !need_pixel && mig_push(V, (uint32_t)glane % kMigBoxes, pix, seg, (uint32_t)s, acc, g, tc, st)) {
         mode = kExit;  // handed over at this sample boundary
         need_sample = false;

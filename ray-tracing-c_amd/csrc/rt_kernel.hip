@@ -1096,7 +1096,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
                         : (lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>),
       b1::kBlock, d->b1_lds_bytes));
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_chain, chain_kernel_fn(lds, cfg.chain_occ), b1::kBlock,
-                                                     d->b1_lds_bytes));
+                                                     d->b1_lds_bytes + b1::kHandoffBytes));
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   const int spill_grid = d->b1_grid > d->chain_grid ? d->b1_grid : d->chain_grid;
@@ -1430,13 +1430,13 @@ static const void *chain_kernel_fn(bool lds, int occ) {
 }
 static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
-  const size_t lds = d->b1_lds_bytes;
+  const size_t lds = d->b1_lds_bytes, bytes = lds + b1::kHandoffBytes;  // (+ the intra-wave cut handoff)
   if (d->cfg.chain_occ == 4) {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 4>), gc, blk, lds, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 4>), gc, blk, 0, st, V, d_out);
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 4>), gc, blk, bytes, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 4>), gc, blk, bytes, st, V, d_out);
   } else {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 5>), gc, blk, lds, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 5>), gc, blk, 0, st, V, d_out);
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 5>), gc, blk, bytes, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 5>), gc, blk, bytes, st, V, d_out);
   }
 }
 
@@ -1539,7 +1539,12 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.ch_sd = d->ch_sd;
   V.rec_count = (unsigned long long *)(d->ch_cnt + kCnRec);
   V.rec_filled = d->ch_cnt + kCnFilled;
-  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // (helpers run cuts too: migration + the LDS scene)
+  V.recut_lanes = cfg.recut ? 1 : 0;  // intra-wave cuts: a lane hands an idle lane of its wave a cut
+  V.recut_min = (uint32_t)cfg.recut_min;
+  V.recut_frac = cfg.recut_frac;
+  V.recut_slack = (uint32_t)cfg.chain_slack;
+  V.recut_stats = d->status + 4;
+  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // helpers cut the chains they run, and run cuts
     V.rq = d->rq;
     V.rq_cap = d->rq_cap;
     V.recut_min = (uint32_t)cfg.recut_min;
@@ -1585,6 +1590,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   b1::Book1View C = V;
   C.n_coop = nullptr;
   C.rq = nullptr;  // (continuation items are whole pixels: nothing to cut)
+  C.recut_lanes = 0;
   C.ch_cont = d->ch_cont;
   C.ch_n_cont = d->ch_cnt + kCnCont;
   C.mig_epoch = ++d->mig_epoch;
