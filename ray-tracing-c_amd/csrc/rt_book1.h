@@ -1575,7 +1575,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
       }
     }
-    if (mode == kExit) continue;
+    if (mode == kExit || mode == kIdle) continue;  // (no item: no new ray)
     // set up the traversal of the new ray
     L.ix = 1.0f / L.dx, L.iy = 1.0f / L.dy, L.iz = 1.0f / L.dz;
     L.a = dot(mk(L.dx, L.dy, L.dz), mk(L.dx, L.dy, L.dz));
