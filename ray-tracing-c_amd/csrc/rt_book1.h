@@ -884,7 +884,7 @@ RT_D uint32_t recut_publish(const Book1View &V, const RecutReq &r) {
     }
     __hip_atomic_store(kdp, (kd & 0xffu) + (ok ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // unlock
   }
-  if (V.recut_stats) at_add(&V.recut_stats[ok ? 0 : 1], 1u);
+  if (V.recut_stats && ok) at_add(&V.recut_stats[0], 1u);  // (declines are not counted: one hot word)
   return ok;
 }
 
@@ -1531,8 +1531,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
             if (t) {
               handoff[(wave_in_block << 6) + __builtin_ctzll(bit)] = make_uint2((uint32_t)pix, t);
               tc |= kWatch;
-            } else {
+            } else {  // (no cut: the pixel's dynamic slots or the records are used up -- do not ask again)
               atomicOr(&idle_lds[wave_in_block], bit);
+              tc |= kNoAsk;
             }
           }
         }
