@@ -639,7 +639,7 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
-  bool recut = true;       // run-time re-cuts in a launch's tail (rt_book1.h: RecutReq)
+  bool recut = false;      // run-time re-cuts in a launch's tail (rt_book1.h: RecutReq; measured slower at N = 8: opt-in)
   int recut_min = 32;      //   of chains with at least this many samples left
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
@@ -1547,10 +1547,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // helpers cut the chains they run, and run cuts
     V.rq = d->rq;
     V.rq_cap = d->rq_cap;
-    V.recut_min = (uint32_t)cfg.recut_min;
-    V.recut_frac = cfg.recut_frac;
-    V.recut_slack = (uint32_t)cfg.chain_slack;
-    V.recut_stats = d->status + 4;
   }
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;

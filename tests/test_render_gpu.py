@@ -373,3 +373,31 @@ def test_dropin_reference_main_on_eight_rehearsed_devices(manifest, tmp_path):
     data = open(os.path.join(str(tmp_path), "output.tiff"), "rb").read()
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
     assert hashlib.sha256(data[168:]).hexdigest() == e["sha256"]
+
+
+# Run-time re-cuts (rt_book1.h: RecutReq; opt-in RT_RECUT=1): in a chain launch's tail a lane hands an
+# idle lane of its wave a cut of its own chain, and helper waves cut the chains they run.
+@pytest.mark.parametrize("env", [
+    {"RT_RECUT": "1"},
+    {**CHAIN, "RT_RECUT": "1", "RT_RECUT_MIN": "4"},
+    {**CHAIN, "RT_RECUT": "1", "RT_RECUT_MIN": "4", "RT_RECUT_FRAC": "0.1"},
+    {**MIGRATE, "RT_RECUT": "1", "RT_RECUT_MIN": "4", "RT_RECUT_FRAC": "0.9"}])
+@pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
+def test_recut_chains_reproduce_reference(manifest, name, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = manifest["renders"][name]
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    _check(img, golden_image(e), f"{name} {env}")
+
+
+def test_recut_north_star_eight_shares(manifest, monkeypatch):
+    """The north-star frame as 8 concurrent shares (rt_render, RT_REHEARSE_DEVICES=8) with re-cuts on:
+    the N = 8 tail is where cuts happen; the frame must be the reference's."""
+    e = manifest["renders"].get("s1_1200x675_1000spp_d50")
+    if e is None:
+        pytest.skip("north-star golden not generated (make_golden.py --big)")
+    monkeypatch.setenv("RT_REHEARSE_DEVICES", "8")
+    monkeypatch.setenv("RT_RECUT", "1")
+    img = rtc.render(rtc.Scene.preset(1, 1200, 1000, 50), n_gpus=8)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"]
