@@ -714,7 +714,37 @@ RT_D float perlin_noise(const rt_perlin &P, f3 p) {  // src/texture.c:78-103
   return value;
 }
 
-RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p) {
+// The general kernel's copy of a scene's single Perlin texture in LDS (rt_general.h): the permutations
+// as bytes (x | y | z, 256 each; host-checked < 256) and the gradients as float4, so the 7 octaves x 8
+// corners of table reads per texture value are LDS reads, not scattered global loads.  Same values,
+// same arithmetic as perlin_noise.
+struct PerlinLds {
+  const uint8_t *perm;
+  const float4 *grad;
+};
+constexpr size_t kPerlinLdsBytes = 3 * 256 + 256 * sizeof(float4);
+RT_D float perlin_noise_lds(const PerlinLds &P, f3 p) {  // src/texture.c:78-103
+  const int i = (int)floorf(p.x), j = (int)floorf(p.y), k = (int)floorf(p.z);
+  const float t1 = p.x - (float)i, t2 = p.y - (float)j, t3 = p.z - (float)k;
+  const float s1 = t1 * t1 * (3.0f - 2.0f * t1);
+  const float s2 = t2 * t2 * (3.0f - 2.0f * t2);
+  const float s3 = t3 * t3 * (3.0f - 2.0f * t3);
+  float value = 0;
+  for (int di = 0; di < 2; di++)
+    for (int dj = 0; dj < 2; dj++)
+      for (int dk = 0; dk < 2; dk++) {
+        const int gi = P.perm[(i + di) & 255] ^ P.perm[256 + ((j + dj) & 255)] ^ P.perm[512 + ((k + dk) & 255)];
+        const float4 gq = P.grad[gi];
+        const f3 grad = mk(gq.x, gq.y, gq.z);
+        const f3 wgt = mk(t1 - (float)di, t2 - (float)dj, t3 - (float)dk);
+        value += dot(grad, wgt) * ((float)di * s1 + (float)(1 - di) * (1.0f - s1)) *
+                 ((float)dj * s2 + (float)(1 - dj) * (1.0f - s2)) * ((float)dk * s3 + (float)(1 - dk) * (1.0f - s3));
+      }
+  return value;
+}
+
+// pl: perlins[0]'s LDS copy (pl.perm null: none)
+RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p, PerlinLds pl = PerlinLds{nullptr, nullptr}) {
   for (int hops = 0; hops < 16; hops++) {
     const rt_texture &t = S.textures[tex];
     if (t.kind == RT_TEX_SOLID) return ld3(t.color);
@@ -738,8 +768,9 @@ RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p) {
     f3 q = scale(p, t.scale);
     const f3 q0 = q;
     float acc = 0.0f, weight = 1.0f;
+    const bool in_lds = pl.perm != nullptr && t.a == 0;
     for (int o = 0; o < P.depth; o++) {
-      acc += weight * perlin_noise(P, q);
+      acc += weight * (in_lds ? perlin_noise_lds(pl, q) : perlin_noise(P, q));
       weight *= 0.5f;
       q = scale(q, 2.0f);
     }
@@ -765,18 +796,19 @@ RT_D f3 onb_local(const Onb &b, f3 a) { return add(add(scale(b.u, a.x), scale(b.
 RT_D f3 reflect(f3 v, f3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
 
 template <int F>
-RT_D f3 emit(const DScene &S, const Rec &r) {  // Material_emit, src/material.c:133-142
+RT_D f3 emit(const DScene &S, const Rec &r, PerlinLds pl = PerlinLds{nullptr, nullptr}) {  // Material_emit, src/material.c:133-142
   if (F & RT_FEAT_EMISSIVE) {
     const rt_material &m = S.materials[r.material];
     if (m.tag == RT_MAT_SURFACE_NORMAL) return scale(add(r.normal, mk(1.0f, 1.0f, 1.0f)), 0.5f);
-    if (m.tag == RT_MAT_DIFFUSE_LIGHT && r.front) return texture_value(S, m.texture, r.u, r.v, r.p);
+    if (m.tag == RT_MAT_DIFFUSE_LIGHT && r.front) return texture_value(S, m.texture, r.u, r.v, r.p, pl);
   }
   return mk(0.0f, 0.0f, 0.0f);
 }
 
 // Material_scatter (src/material.c:103-120).  Returns false when the path ends at this hit.
 template <int F>
-RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 &albedo, bool &skip_pdf) {
+RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 &albedo, bool &skip_pdf,
+                  PerlinLds pl = PerlinLds{nullptr, nullptr}) {
   const rt_material &m = S.materials[r.material];
   switch (m.tag) {
   case RT_MAT_LAMBERTIAN: {  // src/material.c:23-37
@@ -788,14 +820,14 @@ RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 
     rtm::sincosf(phi, &sphi, &cphi);
     const float sq = sqrtf(r2);
     out = onb_local(b, mk(cphi * sq, sphi * sq, sqrtf(1.0f - r2)));
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
     skip_pdf = false;
     return true;
   }
   case RT_MAT_METAL: {  // src/material.c:48-58
     const f3 refl = reflect(normalize(r_in), r.normal);
     out = add(refl, scale(rand_unit_vector(g), m.param));
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
     skip_pdf = true;
     if (dot(out, r.normal) < 0.0f) out = refl;
     return true;
@@ -822,7 +854,7 @@ RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 
   }
   case RT_MAT_ISOTROPIC: {  // src/material.c:93-98
     out = rand_unit_vector(g);
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
     skip_pdf = false;
     return true;
   }

@@ -27,6 +27,7 @@ struct GeneralView {
   int32_t flat;              // kBatch: common entries as one straight-line block (pre_common) plus up to
                              // flat - 1 box entries in the same step (RT_GEN_FLAT; 0: branched dispatch)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
+  int32_t perlin_lds;        // kAllLds: byte offset of perlins[0]'s LDS copy (PerlinLds) behind the preorder; -1: none
 };
 
 // -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
@@ -354,10 +355,22 @@ template <int F, bool kBatch = false, bool kAllLds = false>
 __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, float4 *lds = nullptr) {
   const DScene &S = V.S;
   const uint32_t n_lds = kBatch && lds ? (uint32_t)min(V.n_lds, S.n_pre) : 0u;
+  PerlinLds pl = PerlinLds{nullptr, nullptr};
+  if (kAllLds && V.perlin_lds >= 0) {  // the single Perlin texture's tables, behind the preorder
+    uint8_t *pb = (uint8_t *)lds + V.perlin_lds;
+    float4 *pg = (float4 *)(pb + 3 * 256);
+    const rt_perlin &P = S.perlins[0];
+    for (uint32_t q = threadIdx.x; q < 256; q += blockDim.x) {
+      pb[q] = (uint8_t)P.perm_x[q], pb[256 + q] = (uint8_t)P.perm_y[q], pb[512 + q] = (uint8_t)P.perm_z[q];
+      pg[q] = make_float4(P.grad[q][0], P.grad[q][1], P.grad[q][2], 0.0f);
+    }
+    pl.perm = pb;
+    pl.grad = pg;
+  }
   if (n_lds) {  // the top of the preorder (the first BVH levels of every root item) in LDS
     for (uint32_t q = threadIdx.x; q < 2 * n_lds; q += blockDim.x) lds[q] = S.pre[q];
-    __syncthreads();
   }
+  if (n_lds || pl.perm) __syncthreads();
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
   const int W = S.cam.width;
   const int64_t total = (int64_t)V.n_rows * W;
@@ -576,7 +589,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         make_record<F>(S, o, d, h, r);
         GS_ADD(kGsCycRecord, GS_NOW() - gs_c);
         gs_c = GS_NOW();
-        const f3 e = emit<F>(S, r);
+        const f3 e = emit<F>(S, r, pl);
         GS_ADD(kGsCycEmit, GS_NOW() - gs_c);
         f3 dir, albedo;
         bool skip_pdf;
@@ -594,7 +607,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         GS_ADD(kGsPassPerlin, gs_perlin);
 #endif
         gs_c = GS_NOW();
-        const bool scattered = scatter<F>(S, r, d, g, dir, albedo, skip_pdf);
+        const bool scattered = scatter<F>(S, r, d, g, dir, albedo, skip_pdf, pl);
 #ifdef RT_GEN_STATS
         GS_ADD(gs_perlin ? kGsCycScatterPerlin : kGsCycScatter, GS_NOW() - gs_c);
 #endif

@@ -632,6 +632,7 @@ struct Config {
   float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
   int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
+  bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
@@ -712,6 +713,7 @@ struct Config {
     c.gen_batch = c.gen_batch < 0 ? 0 : (c.gen_batch > 64 ? 64 : c.gen_batch);
     c.gen_lds = env_int("RT_GEN_LDS", 1024);
     c.gen_big = env_flag("RT_GEN_BIG", true);
+    c.gen_perlin = env_flag("RT_GEN_PERLIN_LDS", true);
     c.gen_big_block = env_int("RT_GEN_BIG_BLOCK", c.gen_big_block);
     c.gen_steps = env_int("RT_GEN_STEPS", c.gen_steps);
     if (c.gen_steps < 1) c.gen_steps = 1;
@@ -775,6 +777,8 @@ struct rt_device_scene {
   int gen_grid = 0, gen_block = 256;
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_lds = 0;
+  size_t gen_lds_bytes = 0;   // dynamic LDS of the general kernel
+  int32_t gen_perlin_lds = -1;  // byte offset of the Perlin tables in it, or -1
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1245,13 +1249,21 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   }
   d->gen_lds = lds;
   const bool big = d->gen_block == kBigBlock, big4 = d->gen_block == 1024;
+  size_t lds_bytes = (size_t)lds * 2 * sizeof(float4);
+  // the single Perlin texture's tables in LDS behind the whole preorder, when they fit (scene 7: 158 KiB
+  // of preorder + 4.75 KiB of tables in 160 KiB)
+  d->gen_perlin_lds = -1;
+  if ((big || big4) && cfg.gen_perlin && s->n_perlins == 1 && lds_bytes + kPerlinLdsBytes <= (size_t)prop.sharedMemPerBlock) {
+    d->gen_perlin_lds = (int32_t)lds_bytes;
+    lds_bytes += kPerlinLdsBytes;
+  }
+  d->gen_lds_bytes = lds_bytes;
   const void *fn = big4 ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, 1024>
                               : (const void *)rt_general_kernel<kFeatAll, true, 1024>)
                  : big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
                              : (const void *)rt_general_kernel<kFeatAll, true, kBigBlock>)
                  : batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
                          : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
-  const size_t lds_bytes = (size_t)lds * 2 * sizeof(float4);
   if (lds_bytes > 65536) HIP_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
   int per_cu = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, d->gen_block, lds_bytes));
@@ -1259,8 +1271,9 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   d->gen_grid = prop.multiProcessorCount * per_cu;
   d->general = true;
   if (cfg.debug)
-    fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, features=0x%x\n",
-            d->gen_grid, per_cu, d->gen_block, d->gen_lds, d->view.n_pre, d->features);
+    fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, perlin in lds %d, "
+            "features=0x%x\n", d->gen_grid, per_cu, d->gen_block, d->gen_lds, d->view.n_pre, d->gen_perlin_lds >= 0,
+            d->features);
   return 0;
 }
 
@@ -1719,7 +1732,8 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.rare_min = d->cfg.gen_rare;
   V.flat = d->cfg.gen_flat;
   V.n_lds = d->gen_lds;
-  const size_t lds_bytes = (size_t)d->gen_lds * 2 * sizeof(float4);
+  V.perlin_lds = d->gen_perlin_lds;
+  const size_t lds_bytes = d->gen_lds_bytes;
   if (V.batch && d->gen_block == 1024) {
     const dim3 bb(1024);
     if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, 1024>), g, bb, lds_bytes, st, V, d_out);
