@@ -92,13 +92,6 @@ int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigne
  * (rt_book1_cost_kernel, chain_* planner kernels).  -1 when unavailable. */
 double rt_scene_last_launch_ms(rt_device_scene *dscene);
 
-/* Diagnostics (RT_PX_TIME=1 set at upload time, Book-1 path): for the first n work items of the
- * last launch, times[2k..2k+1] = {start, end} (wall_clock64 ticks, 100 MHz, low 32 bits) and
- * cost[k] = the longest-first pre-pass steps; order[0..n) = the launch's work order and *n_coop = its
- * number of whole-wave items (the first *n_coop of order).  Any output pointer may be NULL. */
-int rt_scene_px_time(rt_device_scene *dscene, uint32_t *times, uint32_t *cost, int32_t *order, uint32_t *n_coop,
-                     int64_t n);
-
 /* Diagnostics (RT_PX_TIME=1 set at upload time): the last chain launch, one row of 16 uint32 per work
  * item in item order: pixel, segment, K, whole-wave (1) / lane (0), start, end (wall_clock64 ticks,
  * 100 MHz, low 32 bits), records written (samples for segment 0 / unsplit), flags (bit 0 coupled,

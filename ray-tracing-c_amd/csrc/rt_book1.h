@@ -10,7 +10,7 @@
 //  * the path record is a list of material ids (albedo of a Solid texture is a function of the
 //    material) in registers (two 4-id chunks) + a per-lane global spill area for deep paths; the
 //    colour is folded innermost-first at path end exactly like the recursion;
-//  * the heaviest work items run on whole waves (render_wave_items) next to the lane kernel;
+//  * the heaviest chain items run on whole waves (coop_items) in the chain kernel's first waves;
 //  * chain render (kMode 2): a pixel's sample stream can be cut into segments that run as separate
 //    work items and meet again exactly (ChainPx below) -- the frame is no longer bound by the
 //    longest pixel's sequential chain when it is split over many GPUs.
@@ -156,21 +156,16 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
-  const int32_t *order;      // work item order (longest-first from the cost pre-pass), or null
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
-  uint32_t sample_cost;      // cost pre-pass: traversal-step equivalent of one sample's fixed latency
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
-  const uint32_t *n_coop;    // the first *n_coop items (of `order` / ch_items) go to whole waves
-  int32_t *coop_counter;     //   (render_pixel_coop), claimed through this counter
+  const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
+  int32_t *coop_counter;     //   (coop_items), claimed through this counter
   const uint32_t *coop_waves_dev;  // by the first *coop_waves_dev waves of the grid
   uint64_t *spill;           // [chunk][global lane]: a deep path's older 4-id chunks (Record)
   int32_t spill_lanes;
   int32_t n_bf_leaves;       // whole-wave pixels: leaves for bf_candidate; 0: off (coop_trace9 instead)
   uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end}, wall_clock64 low bits
-  const uint4 *wide;         // group trace (rt_group.h): 8-entry treelets over the preorder items
-  int32_t n_wide;            // 0: group kernel unavailable for this scene
-  const uint16_t *anc;       // group trace: [item][16] ancestor item positions of each leaf (0xffff: none)
   // chain render (kMode 2)
   const ChainPx *ch_px;      // per pixel
   const uint2 *ch_items;     // {pixel, segment | kItemUnsplit}: whole-wave items first, then lanes'
@@ -1193,40 +1188,6 @@ __device__ __attribute__((noinline)) void coop_items(const Book1View &V, const f
   }
 }
 
-// The whole-wave kernel (rt_book1_wave_kernel), launched on a second stream next to the lane kernel:
-// its first *coop_waves_dev waves claim the first *n_coop items, one item per wave, heaviest first.
-// A kernel of its own, so that the whole-wave code's registers do not count against the lane
-// kernel's occupancy; the lane kernel leaves it the same number of workgroups.
-template <bool kLds, int kMode>
-__device__ void render_wave_items(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
-  const int waves = (int)*V.coop_waves_dev;
-  if ((int)blockIdx.x * kWaves >= waves) return;  // whole workgroup: before the barrier
-  float4 *items9 = (float4 *)lds;
-  if (kLds) {
-    for (int q = threadIdx.x; q < 2 * V.n_items9_alloc; q += kBlock) items9[q] = V.items9_g[q];
-    __syncthreads();
-  } else {
-    items9 = (float4 *)V.items9_g;
-  }
-  const int wave = (int)(blockIdx.x * kBlock + threadIdx.x) / 64;
-  if (wave >= waves) return;
-  const int64_t n_coop = (int64_t)*V.n_coop;
-  for (;;) {
-    int k = 0;
-    if (__lane_id() == 0) k = atomicAdd(V.coop_counter, 1);
-    k = __shfl(k, 0);
-    if (k >= n_coop) break;
-    __builtin_amdgcn_s_setprio(3);  // these chains set the frame time: issue before the lane-parallel waves
-    if (kMode == 2) {
-      const uint2 it = V.ch_items[k];
-      render_item_coop<2>(V, items9, (int64_t)it.x, it.y, out);
-    } else {
-      render_item_coop<0>(V, items9, (int64_t)V.order[k], 0u, out);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-}
-
 // kIdle: a chain-launch lane with no work item left; a lane of its wave may hand it a cut (below)
 enum : int { kTrav = 0, kWait = 1, kExit = 2, kIdle = 3 };
 // LDS behind the scene items (chain launches): per lane a handed-over cut {pixel, segment} (segment 0:
@@ -1242,11 +1203,6 @@ constexpr int kSteps = 16;
 template <bool kLds, int kMode = 0>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
-  // lane launches: the last workgroups of the grid leave their CU slots to the whole-wave kernel
-  // (render_wave_items); chain launches run their whole-wave items in the grid's first waves (below)
-  if (kMode != 2 && V.n_coop != nullptr &&
-      (int)blockIdx.x >= (int)gridDim.x - (int)((*V.coop_waves_dev + kWaves - 1) / kWaves))
-    return;
   const bool cont = kMode == 2 && V.ch_cont != nullptr;
   if (cont && *V.ch_n_cont == 0u) return;  // (before staging the scene: the usual continuation launch is empty)
   const int W = V.S.cam.width;
@@ -1317,9 +1273,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   L.hit = -1;
   L.cur = 0;
 
-  // the heaviest items (the first *n_coop) are rendered by whole waves in the concurrent
-  // rt_book1_wave_kernel (render_wave_items); the lanes' own items start after them
-  const int64_t work_offset = V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
+  // chain launches: the heaviest items (the first *n_coop) run on whole waves (coop_items); the lanes'
+  // own items start after them
+  const int64_t work_offset = kMode == 2 && V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   const int64_t total_own = cont ? (int64_t)*V.ch_n_cont
                             : kMode == 2 ? (int64_t)*V.ch_n_items - work_offset
                                          : total - work_offset;
@@ -1421,10 +1377,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          // (+ a per-sample constant: a sample's latency is ~sample_cost traversal steps beyond its own
-          // steps -- camera ray, shading passes, batch waits; fitted on chain timelines)
           if (kMode == 1)
-            V.cost_out[pix] = (cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps) + V.sample_cost * (uint32_t)spp;
+            V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
           if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
@@ -1491,7 +1445,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           pix = (int32_t)it.x;
           seg = it.y;
         } else {
-          pix = V.order ? V.order[item + work_offset] : (int32_t)(item + work_offset);  // longest first
+          pix = (int32_t)item;  // (lane launches: low spp / small images, in pixel order)
         }
         {
           const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;

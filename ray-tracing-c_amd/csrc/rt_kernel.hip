@@ -7,10 +7,8 @@
 // writes its own compact rows.
 //
 // Kernels (rt_scene_kernel names the frame kernel of a scene):
-//   rt_book1_kernel        Book-1 scenes, lane = pixel, longest-first order (RT_MODE=lane)
 //   rt_book1_chain_kernel  Book-1 scenes, lane = chain segment (default); chain_* planner / fold
-//   rt_book1_wave_kernel   the heaviest items on whole waves, concurrent on a second stream
-//   rt_book1_group_kernel  eight lanes per pixel (RT_MODE=group)
+//   rt_book1_kernel        Book-1 scenes at low spp / small images, lane = pixel (or RT_MODE=lane)
 //   rt_book1_cost_kernel   the low-spp pre-pass that measures every pixel's cost
 //   rt_general_kernel      every other scene (Book-2 features)
 // Every tuning knob (RT_* environment variables) is read once, at scene upload.
@@ -30,7 +28,6 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_book1.h"
-#include "rt_group.h"
 #include "rt_general.h"
 #include "rt_device.h"
 
@@ -86,34 +83,24 @@ __global__ __launch_bounds__(kBlock) void rt_render_deep_kernel(DScene S, int ro
   }
 }
 
-// Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.
-template <bool kLds, int kOcc = 5>
-__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+// Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.  The
+// chain kernel and its cost pre-pass run at 4 waves per SIMD (128 VGPRs: no spills in the loop; 5 waves
+// spilled and measured slower); the lane kernel at 5.
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
-template <bool kLds, int kOcc = 5>
-__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock, 4) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 2>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
-template <bool kLds, int kOcc = 5>
-__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds>
+__global__ __launch_bounds__(b1::kBlock, 4) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 1>(V, out, lds);
-}
-// The group kernel (rt_group.h): eight lanes per pixel.
-template <bool kLds>
-__global__ __launch_bounds__(grp::kBlock) void rt_book1_group_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  grp::render_groups<kLds>(V, out, lds);
-}
-// The whole-wave items of a Book-1 launch (rt_book1.h: render_wave_items), on a second stream.
-template <bool kLds, int kMode>
-__global__ __launch_bounds__(b1::kBlock) void rt_book1_wave_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  b1::render_wave_items<kLds, kMode>(V, out, lds);
 }
 // After a chain launch: one wave per split pixel (rt_book1.h: chain_fold).
 __global__ __launch_bounds__(256) void chain_fold_kernel(b1::Book1View V, uint8_t *__restrict__ out,
@@ -250,69 +237,23 @@ __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist, uns
   }
 }
 
-// Cost model of one launch, in clocks per pre-pass step (fitted on the headline frame, DESIGN.md
-// §5): the launch ends when the slowest lane chain (lat_step), the lanes' aggregate work (thr_step
-// per lane), the whole-wave queue and the heaviest whole-wave chain (coop_step) are all done.
-// LPT scratch (u32): 256 bucket counts, 256 running offsets, 4 split counters [512..515], then from
-// u32 544 the 256 per-bucket step sums (u64).
+// LPT scratch (u32): 256 bucket counts, 256 running offsets, then from u32 544 the 256 per-bucket
+// step sums (u64).
 constexpr size_t kLptHistBytes = 8192;
 
-struct LptModel {
-  float spp_ratio;  // frame spp / pre-pass spp (costs are pre-pass steps)
-  int grid_waves;
-  float lat_step;   // clocks per step of the slowest lane (group) pixels under load: their chain
-  float thr_step;   // clocks per step per lane (group) of all lanes' (groups') aggregate rate
-  float coop_step;  // clocks per step of a whole-wave pixel (its chain, and its wave's rate)
-  int lanes_per_wave;  // pixels in flight per non-cooperative wave: 64 lanes, or 8 groups
-};
-// clocks per pre-pass step, fitted to frame times on one MI355X (scripts/tail_probe.py measures the
-// per-pixel rates: lane pixels ~1.6-4k by load, group ~0.6-1.1k, whole-wave ~120-180)
-constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kGroupLat = 850.0f, kGroupThr = 850.0f;
-constexpr float kCoopStep = 180.0f, kCoopStepLane = 250.0f;
+// Per-step clock rates of the chain kernel under load, fitted to frame times on one MI355X (DESIGN.md
+// §5): the slowest lane chain's latency and the lanes' aggregate throughput per pre-pass traversal
+// step, and a whole-wave chain's rate.
+constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
 
-// one thread: offsets, highest bucket first; hist[512] = items in buckets above the chosen split
-// (rendered by whole waves), hist[513] = their claim counter, hist[515] = whole waves.
-// coop_bucket / coop_waves < 0: chosen by the model.
-__global__ void lpt_scan_kernel(uint32_t *hist, const unsigned long long *sums, int coop_bucket, int coop_waves,
-                                LptModel m) {
+// one thread: running offsets, highest bucket first (longest first)
+__global__ void lpt_scan_kernel(uint32_t *hist) {
   if (threadIdx.x != 0) return;
   uint32_t run = 0;
   for (int k = 255; k >= 0; k--) {
     hist[256 + k] = run;
     run += hist[k];
   }
-  double total = 0.0;
-  for (int k = 0; k < 256; k++) total += (double)sums[k];
-  int best_b = coop_bucket >= 0 ? coop_bucket : 255, best_w = coop_waves >= 0 ? coop_waves : 0;
-  if (coop_bucket < 0 || coop_waves < 0) {
-    // highest non-empty bucket at or below each bucket (the largest lane pixel of a split)
-    int16_t top_of[256];
-    for (int k = 0, t = -1; k < 256; k++) top_of[k] = (int16_t)(t = hist[k] ? k : t);
-    const double top_all = top_of[255] < 0 ? 0.0
-                                           : ldexp((double)(9 + (top_of[255] & 7)) / 8.0, top_of[255] >> 3) * m.spp_ratio;
-    double best_t = 1e300;
-    for (int wc = 0; wc <= m.grid_waves / 2; wc = wc ? 2 * wc : 128) {
-      if (coop_waves >= 0 && wc != coop_waves) continue;
-      double coop_work = 0.0;  // steps above the split
-      for (int b = 255; b >= -1; b--) {
-        if (b < 255) coop_work += (double)sums[b + 1];
-        if (coop_bucket >= 0 && b != coop_bucket) continue;
-        if (wc == 0 && coop_work > 0.0) break;
-        const int top = b < 0 ? -1 : top_of[b];
-        const double maxc = top < 0 ? 0.0 : ldexp((double)(9 + (top & 7)) / 8.0, top >> 3) * m.spp_ratio;
-        const double lanes = (double)(m.grid_waves - wc) * m.lanes_per_wave;
-        const double t_dfs = fmax(maxc * m.lat_step, (total - coop_work) * m.spp_ratio * m.thr_step / lanes);
-        const double t_coop = wc ? fmax(coop_work * m.spp_ratio * m.coop_step / wc, top_all * m.coop_step) : 0.0;
-        const double t = fmax(t_dfs, t_coop);
-        if (t < best_t) best_t = t, best_b = b, best_w = wc;
-      }
-    }
-  }
-  uint32_t coop = 0;
-  for (int k = 255; k > best_b; k--) coop += hist[k];
-  hist[512] = best_w > 0 ? coop : 0;
-  hist[513] = 0;
-  hist[515] = (uint32_t)best_w;
 }
 
 __global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order) {
@@ -320,10 +261,10 @@ __global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, 
     order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
 }
 
-// The whole-wave items (the first hist[512] of the order) exactly longest first: the buckets keep
-// an arbitrary order among items of up to 12.5 % different cost, and with a few whole waves per
-// hundred items the heaviest pixel could start only after a wave's first item (measured at N = 8:
-// started at 72 ms, the frame's last item).  One workgroup, bitonic sort (descending) in LDS.
+// Bitonic sort (descending) in LDS, one workgroup: the chain planner's whole-wave items exactly
+// longest first (the buckets keep an arbitrary order among items of up to 12.5 % different cost, and
+// with a few whole waves per hundred items the heaviest pixel could start only after a wave's first
+// item: measured at N = 8, started at 72 ms, the frame's last item).
 template <typename K, typename T>
 __device__ void bitonic_desc(K *key, T *val, int m) {
   for (int k = 2; k <= m; k <<= 1)
@@ -343,23 +284,6 @@ __device__ void bitonic_desc(K *key, T *val, int m) {
       __syncthreads();
     }
 }
-constexpr int kCoopSort = 8192;  // 64 KB of LDS
-__global__ __launch_bounds__(1024) void lpt_coop_sort_kernel(const uint32_t *cost, const uint32_t *hist, int32_t *order) {
-  __shared__ uint32_t key[kCoopSort];
-  __shared__ int32_t val[kCoopSort];
-  const int n = (int)min(hist[512], (uint32_t)kCoopSort);
-  if (n < 2) return;
-  int m = 2;
-  while (m < n) m <<= 1;
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    key[i] = i < n ? cost[order[i]] : 0u;  // padding sorts last
-    val[i] = i < n ? order[i] : -1;
-  }
-  __syncthreads();
-  bitonic_desc(key, val, m);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) order[i] = val[i];
-}
-
 // ------------------------------------------------------------------------------ chain planner
 // Device-side plan of a chain launch (rt_book1.h: ChainPx), after the cost pre-pass and lpt_hist:
 //   chain_params_kernel   the lane chain target c* (pre-pass steps) from the launch's total work;
@@ -374,7 +298,7 @@ __global__ __launch_bounds__(1024) void lpt_coop_sort_kernel(const uint32_t *cos
 enum : int {
   kCnItems = 0, kCnSplit = 1, kCnFilled = 2, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
   kCnCoopWaves = 7, kCnCoopCounter = 8, kCnNCoop = 9, kCnWaveWork = 10 /* u64 */, kCnCstar = 12, kCnCstarW = 13,
-  kCnHist = 256, kCnOff = 512, kCnCstarTab = 768, kCnWords = 1024
+  kCnHist = 256, kCnOff = 512, kCnWords = 1024
 };
 
 struct ChainModel {
@@ -382,7 +306,6 @@ struct ChainModel {
   int grid_waves;       // waves of the lane kernel's grid
   float lat, thr, coop; // clocks per pre-pass step: lane chain latency, per-lane throughput, whole wave
   float beta;           // a lane chain's latency target, as a fraction of the launch's throughput time
-  float floor_beta;     // > 0: per cost bucket, the time left after the heavier buckets (chain_params_kernel)
   float margin;         // records per segment: margin * spp / K + slack
   int slack;
   int kmax_lane, kmax_wave;
@@ -403,16 +326,6 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
   const float cstar = (float)fmax(1.0, m.beta * total * m.thr / (lanes * m.lat));
   cnt[kCnCstar] = __float_as_uint(cstar);
   cnt[kCnCstarW] = __float_as_uint(cstar * m.lat / m.coop);
-  // per cost bucket: lanes take pixels heaviest first, so a pixel of bucket b starts once the work
-  // of the heavier buckets is done (t_b = W_above(b) / throughput) and has T - t_b left before the
-  // launch's throughput time T: its chains get that slack, not T (floor: m.floor_beta * T)
-  double above = 0.0;
-  for (int b = 255; b >= 0; b--) {
-    const double left = fmax(m.beta * (total - above), m.floor_beta * total);
-    const float cb = m.floor_beta > 0.0f ? (float)fmax(1.0, left * m.thr / (lanes * m.lat)) : cstar;
-    cnt[kCnCstarTab + b] = __float_as_uint(cb);
-    above += (double)sums[b];
-  }
 }
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
@@ -425,8 +338,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
   __syncthreads();
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     const uint32_t c = cost[p];
-    const float cstar = __uint_as_float(cnt[kCnCstarTab + lpt_bucket(c)]);
-    const float cstar_w = cstar * m.lat / m.coop;
+    const float cstar = __uint_as_float(cnt[kCnCstar]), cstar_w = __uint_as_float(cnt[kCnCstarW]);
     int K = (int)fminf(ceilf((float)c / cstar), 1e6f);
     bool wave = false;
     if (K > m.kmax_lane && m.kmax_wave > 0) {  // too long for lane chains: whole-wave chains
@@ -614,26 +526,22 @@ static float env_float(const char *name, float dflt) {
   return (e && *e) ? (float)atof(e) : dflt;
 }
 
-enum : int { kModeLane = 0, kModeGroup = 1, kModeChain = 2, kModeAuto = 3 };
+enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 
 // Every knob, read once per scene upload (INTEGRATION.md lists them).
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
-  bool lpt = true, bf = true, coop_sort = true, wave_prio = true, px_time = false, debug = false;
-  int lpt_spp = 16, coop_steps = -1, coop_waves = -1, shade_batch = 48;
+  bool lpt = true, bf = true, px_time = false, debug = false;
+  int lpt_spp = 16, shade_batch = 48;
   int mode = kModeAuto;
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
   float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
-  float chain_floor = 0.0f;  // > 0: per-bucket chain targets (measured: N=2/4 +2-5 %, N=1/8 -7 %; off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
-  float lane_lat = kLaneLat, lane_thr = kLaneThr, lane_coop = kCoopStepLane;
-  float group_lat = kGroupLat, group_thr = kGroupThr, group_coop = kCoopStep;
   int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
-  int gen_big_block = 768;
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
@@ -643,18 +551,11 @@ struct Config {
   bool recut = false;      // run-time re-cuts in a launch's tail (rt_book1.h: RecutReq; measured slower at N = 8: opt-in)
   int recut_min = 32;      //   of chains with at least this many samples left
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
-  int chain_occ = 4;  // chain kernel occupancy target (waves per SIMD: 4 or 5)
-  int lane_occ = 5;   // lane kernel occupancy target
-  int sample_cost = 0;     // cost pre-pass: per-sample latency in traversal steps (measured: 75-250 slower; off)
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
-    c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ) == 5 ? 5 : 4;
-    c.lane_occ = env_int("RT_LANE_OCC", c.lane_occ) == 4 ? 4 : 5;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
-    c.sample_cost = env_int("RT_SAMPLE_COST", c.sample_cost);
-    if (c.sample_cost < 0) c.sample_cost = 0;
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -675,19 +576,14 @@ struct Config {
     c.gen_pre = env_flag("RT_GEN_PRE", true);
     c.lpt = env_flag("RT_LPT", true);
     c.bf = env_flag("RT_BF", true);
-    c.coop_sort = env_flag("RT_COOP_SORT", true);
-    c.wave_prio = env_flag("RT_WAVE_PRIO", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
     c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
     if (c.lpt_spp < 1) c.lpt_spp = 1;
-    c.coop_steps = env_int("RT_COOP_STEPS", -1);
-    c.coop_waves = env_int("RT_COOP_WAVES", -1);
     c.shade_batch = env_int("RT_SHADE_BATCH", 48);
     c.shade_batch = c.shade_batch < 1 ? 1 : (c.shade_batch > 64 ? 64 : c.shade_batch);  // >= 1: progress
     if (const char *m = getenv("RT_MODE")) {
       if (!strcmp(m, "lane")) c.mode = kModeLane;
-      else if (!strcmp(m, "group")) c.mode = kModeGroup;
       else if (!strcmp(m, "chain")) c.mode = kModeChain;
     }
     c.chain_beta = env_float("RT_CHAIN_BETA", c.chain_beta);
@@ -703,18 +599,14 @@ struct Config {
     c.chain_smooth = env_int("RT_CHAIN_SMOOTH", c.chain_smooth);
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
-    c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
-    if (const char *e = getenv("RT_MODEL_LANE")) sscanf(e, "%f,%f,%f", &c.lane_lat, &c.lane_thr, &c.lane_coop);
-    if (const char *e = getenv("RT_MODEL_GROUP")) sscanf(e, "%f,%f,%f", &c.group_lat, &c.group_thr, &c.group_coop);
     c.gen_batch = env_int("RT_GEN_BATCH", 56);
     c.gen_batch = c.gen_batch < 0 ? 0 : (c.gen_batch > 64 ? 64 : c.gen_batch);
     c.gen_lds = env_int("RT_GEN_LDS", 1024);
     c.gen_big = env_flag("RT_GEN_BIG", true);
     c.gen_perlin = env_flag("RT_GEN_PERLIN_LDS", true);
-    c.gen_big_block = env_int("RT_GEN_BIG_BLOCK", c.gen_big_block);
     c.gen_steps = env_int("RT_GEN_STEPS", c.gen_steps);
     if (c.gen_steps < 1) c.gen_steps = 1;
     c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
@@ -752,10 +644,6 @@ struct rt_device_scene {
   uint32_t mig_epoch = 0;        //   its entries are tagged with a per-launch epoch
   uint32_t *px_time = nullptr;   // RT_PX_TIME diagnostic: {start, end} per work item
   uint32_t *seg_time = nullptr;  //   and per chain segment
-  int g_grid = 0;                // group kernel: resident workgroups, LDS bytes per workgroup
-  size_t g_lds_bytes = 0;
-  hipStream_t wave_stream = nullptr;  // the whole-wave kernel's stream (forked from / joined to the caller's)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // chain render scratch (rt_book1.h: ChainPx), sized for the whole frame at upload; records on demand
   void *ch_arena = nullptr;
   uint32_t *ch_cnt = nullptr, *ch_k = nullptr, *ch_split = nullptr;
@@ -877,8 +765,6 @@ struct HostPack {
   bool book1 = false;
   std::vector<float4> items9;     // Book-1: the world in traversal preorder (rt_book1.h: trav_step_v9)
   int n_bf = 0;                   // leaves for the whole-wave candidate trace (0: off)
-  std::vector<uint4> wide;        // group trace treelets (rt_group.h)
-  std::vector<uint16_t> anc;      // group trace: per-leaf ancestors
   std::vector<b1::FastMat> mats;
   std::vector<float4> pre;        // general path preorder (rt_device.h: build_preorder)
 };
@@ -908,7 +794,7 @@ static bool book1_eligible(const rt_flat_scene *s, const Config &cfg) {
   return true;
 }
 
-// Book-1 arrays: the preorder items, the group treelets and ancestor table, the materials.
+// Book-1 arrays: the preorder items and the materials.
 static void book1_pack(const rt_flat_scene *s, HostPack &H) {
   const rt_list &root = s->lists[rt_ref_index(s->root)];
   std::vector<float4> &items9 = H.items9;
@@ -950,101 +836,6 @@ static void book1_pack(const rt_flat_scene *s, HostPack &H) {
       h.w = bits_as_float(bf_item[n]);
   }
   H.n_bf = !bf_item.empty() && bf_item.size() <= (size_t)64 * b1::kBfSlots && H.cfg.bf ? (int)bf_item.size() : 0;
-  // group trace treelets (rt_group.h): greedy treelets of <= 8 entries over the preorder items, each
-  // entry with <= 3 opened internal nodes between it and the treelet's (already tested) root; and the
-  // per-leaf ancestor table for the winner's check
-  std::vector<uint4> &wide = H.wide;
-  std::vector<uint16_t> &anc = H.anc;
-  {
-    const int n_items = (int)(items9.size() / 2) - 1;  // without the pad item
-    auto is_leaf = [&](int p) {
-      uint32_t w;
-      memcpy(&w, &items9[2 * p + 1].w, 4);
-      return (w & b1::kLeaf9) != 0;
-    };
-    auto size_of = [&](int p) {
-      if (is_leaf(p)) return 1;
-      uint32_t k;
-      memcpy(&k, &items9[2 * p + 1].z, 4);
-      return (int)k;
-    };
-    auto kids = [&](int p, int out[2]) {
-      const int l = p + 1;
-      int n = 0;
-      out[n++] = l;
-      if (l + size_of(l) < p + size_of(p)) out[n++] = l + size_of(l);
-      return n;
-    };
-    struct E {
-      int item, n_chain;
-      uint32_t need;
-    };
-    bool ok = n_items > 0 && n_items < 0xffff;
-    std::function<int(const std::vector<int> &)> make = [&](const std::vector<int> &level1) -> int {
-      if (!ok || level1.size() > (size_t)grp::kG) return ok = false, -1;
-      std::vector<E> es;
-      std::vector<int> internals;
-      for (int c : level1) es.push_back({c, 0, 0u});
-      for (;;) {  // open the internal entry with the largest subtree while the treelet has room
-        int pick = -1;
-        for (int k = 0; k < (int)es.size(); k++) {
-          int kc[2];
-          if (is_leaf(es[k].item) || es[k].n_chain >= 3 || (int)es.size() + kids(es[k].item, kc) - 1 > grp::kG)
-            continue;
-          if (pick < 0 || size_of(es[k].item) > size_of(es[pick].item)) pick = k;
-        }
-        if (pick < 0 || (int)internals.size() >= grp::kG) break;
-        const E old = es[pick];
-        int kc[2];
-        const int nc = kids(old.item, kc);
-        const uint32_t bit = 1u << internals.size();
-        internals.push_back(old.item);
-        std::vector<E> repl;
-        for (int c = 0; c < nc; c++) repl.push_back({kc[c], old.n_chain + 1, old.need | bit});
-        es.erase(es.begin() + pick);
-        es.insert(es.begin() + pick, repl.begin(), repl.end());
-      }
-      const int id = (int)(wide.size() / grp::kG);
-      for (int k = 0; k < grp::kG; k++)
-        wide.push_back(make_uint4(grp::kEmpty, 0u, 0u, k < (int)internals.size() ? (uint32_t)internals[k] : grp::kEmpty));
-      for (int k = 0; k < (int)es.size(); k++) {
-        const E &e = es[k];
-        uint32_t child = 0;
-        if (!is_leaf(e.item)) {
-          int kc[2];
-          const int nc = kids(e.item, kc);
-          const int c = make(std::vector<int>(kc, kc + nc));
-          if (c < 0) return -1;
-          child = (uint32_t)c;
-        }
-        uint4 &w = wide[(size_t)id * grp::kG + k];
-        w.x = (uint32_t)e.item, w.y = child, w.z = e.need | (is_leaf(e.item) ? 0x100u : 0u);
-      }
-      return id;
-    };
-    std::vector<int> tops;
-    for (int p = 0; p < n_items; p += size_of(p)) tops.push_back(p);
-    if (make(tops) != 0 || !ok) wide.clear();
-    if (!wide.empty()) {  // ancestors of every leaf, root first
-      anc.assign((size_t)(n_items + 1) * grp::kMaxAnc, 0xffffu);
-      std::vector<int> path;
-      std::function<void(int)> walk = [&](int p) {
-        if (!ok) return;
-        if (is_leaf(p)) {
-          if ((int)path.size() > grp::kMaxAnc) return void(ok = false);
-          for (size_t q = 0; q < path.size(); q++) anc[(size_t)p * grp::kMaxAnc + q] = (uint16_t)path[q];
-          return;
-        }
-        path.push_back(p);
-        int kc[2];
-        const int nc = kids(p, kc);
-        for (int c = 0; c < nc; c++) walk(kc[c]);
-        path.pop_back();
-      };
-      for (int t : tops) walk(t);
-      if (!ok) wide.clear(), anc.clear();
-    }
-  }
   H.mats.resize(s->n_materials);
   for (int k = 0; k < s->n_materials; k++) {
     const rt_material &m = s->materials[k];
@@ -1084,7 +875,6 @@ extern "C" int rt_device_count(void) {
 extern "C" void rt_scene_release(rt_device_scene *d);
 
 // Book-1 device state: the pack's arrays, the persistent grids, the LPT and chain scratch.
-static const void *chain_kernel_fn(bool lds, int occ);
 
 static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPack &H) {
   const Config &cfg = d->cfg;
@@ -1095,12 +885,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
   int per_cu = 0, per_cu_chain = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu,
-      cfg.lane_occ == 4 ? (lds ? (const void *)rt_book1_kernel<true, 4> : (const void *)rt_book1_kernel<false, 4>)
-                        : (lds ? (const void *)rt_book1_kernel<true, 5> : (const void *)rt_book1_kernel<false, 5>),
-      b1::kBlock, d->b1_lds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_chain, chain_kernel_fn(lds, cfg.chain_occ), b1::kBlock,
-                                                     d->b1_lds_bytes + b1::kHandoffBytes));
+      &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock,
+      d->b1_lds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
+      b1::kBlock, d->b1_lds_bytes + b1::kHandoffBytes));
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   const int spill_grid = d->b1_grid > d->chain_grid ? d->b1_grid : d->chain_grid;
@@ -1109,14 +898,13 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   const int chunks = (s->camera.max_depth + 3) / 4 - 2;
   const size_t spill_bytes = (size_t)(chunks > 0 ? chunks : 0) * spill_lanes * sizeof(uint64_t);
   const size_t npix = (size_t)s->camera.width * s->camera.height;
-  const size_t sizes[10] = {items_bytes, H.mats.size() * sizeof(b1::FastMat), kCounterSlot, spill_bytes,
-                            npix * sizeof(uint32_t),   // [4] pre-pass cost
-                            npix * sizeof(int32_t),    // [5] LPT order
-                            kLptHistBytes,             // [6] LPT buckets
-                            H.wide.size() * sizeof(uint4), H.anc.size() * sizeof(uint16_t),  // [7] [8] group
-                            npix * sizeof(uint32_t)};  // [9] pre-pass draws
-  size_t off[10], total = 0;
-  for (int k = 0; k < 10; k++) {
+  const size_t sizes[8] = {items_bytes, H.mats.size() * sizeof(b1::FastMat), kCounterSlot, spill_bytes,
+                           npix * sizeof(uint32_t),   // [4] pre-pass cost
+                           npix * sizeof(int32_t),    // [5] LPT order
+                           kLptHistBytes,             // [6] LPT buckets
+                           npix * sizeof(uint32_t)};  // [7] pre-pass draws
+  size_t off[8], total = 0;
+  for (int k = 0; k < 8; k++) {
     off[k] = total;
     total = align_up(total + (sizes[k] ? sizes[k] : 16), 256);
   }
@@ -1126,8 +914,6 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   char *b = (char *)arena;
   HIP_OK(hipMemcpy(b + off[0], H.items9.data(), sizes[0], hipMemcpyHostToDevice));
   if (sizes[1]) HIP_OK(hipMemcpy(b + off[1], H.mats.data(), sizes[1], hipMemcpyHostToDevice));
-  if (sizes[7]) HIP_OK(hipMemcpy(b + off[7], H.wide.data(), sizes[7], hipMemcpyHostToDevice));
-  if (sizes[8]) HIP_OK(hipMemcpy(b + off[8], H.anc.data(), sizes[8], hipMemcpyHostToDevice));
   b1::Book1View &V = d->b1view;
   memset(&V, 0, sizeof V);
   V.S = d->view;
@@ -1148,28 +934,10 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.spill_lanes = spill_lanes;
   V.shade_batch = cfg.shade_batch;
   V.n_bf_leaves = H.n_bf;
-  V.wide = (const uint4 *)(b + off[7]);
-  V.n_wide = (int32_t)(H.wide.size() / grp::kG);
-  V.anc = (const uint16_t *)(b + off[8]);
   d->lpt_cost = (uint32_t *)(b + off[4]);
   d->lpt_order = (int32_t *)(b + off[5]);
   d->lpt_hist = (uint32_t *)(b + off[6]);
-  d->draw_out = (uint32_t *)(b + off[9]);
-  if (V.n_wide > 0) {  // the group kernel (rt_group.h)
-    d->g_lds_bytes = align_up((lds ? items_bytes : 0) + (size_t)grp::kGroups * grp::kStack * sizeof(uint32_t), 16);
-    int per = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, lds ? (const void *)rt_book1_group_kernel<true> : (const void *)rt_book1_group_kernel<false>,
-        grp::kBlock, d->g_lds_bytes));
-    d->g_grid = prop.multiProcessorCount * (per < 1 ? 1 : per);
-    if (d->g_grid * grp::kGroups > spill_lanes) d->g_grid = spill_lanes / grp::kGroups;  // record spill columns
-  }
-  // the whole-wave kernel's stream: high priority, its workgroups take CU slots ahead of the lanes'
-  int prio_lo = 0, prio_hi = 0;
-  HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HIP_OK(hipStreamCreateWithPriority(&d->wave_stream, hipStreamNonBlocking, cfg.wave_prio ? prio_hi : prio_lo));
-  HIP_OK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+  d->draw_out = (uint32_t *)(b + off[7]);
   if (cfg.px_time) {
     HIP_OK(hipMalloc(&d->px_time, npix * 2 * sizeof(uint32_t)));
     V.px_time = d->px_time;
@@ -1210,8 +978,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   }
   d->book1 = true;
   if (cfg.debug)
-    fprintf(stderr, "[rtc] book1 lds=%d bytes=%zu grid=%d chain_grid=%d group_grid=%d bf=%d spill_chunks=%d\n", (int)lds,
-            d->b1_lds_bytes, d->b1_grid, d->chain_grid, d->g_grid, H.n_bf, chunks);
+    fprintf(stderr, "[rtc] book1 lds=%d bytes=%zu grid=%d chain_grid=%d bf=%d spill_chunks=%d\n", (int)lds,
+            d->b1_lds_bytes, d->b1_grid, d->chain_grid, H.n_bf, chunks);
   return 0;
 }
 
@@ -1244,23 +1012,21 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const size_t pre_bytes = (size_t)d->view.n_pre * 2 * sizeof(float4);
   d->gen_block = gen::kBlock;
   if (batch && cfg.gen_big && d->view.n_pre > lds && pre_bytes <= (size_t)prop.sharedMemPerBlock) {
-    d->gen_block = cfg.gen_big_block == 1024 ? 1024 : kBigBlock;  // the whole preorder in one workgroup's LDS
+    d->gen_block = kBigBlock;  // the whole preorder in one workgroup's LDS
     lds = d->view.n_pre;
   }
   d->gen_lds = lds;
-  const bool big = d->gen_block == kBigBlock, big4 = d->gen_block == 1024;
+  const bool big = d->gen_block == kBigBlock;
   size_t lds_bytes = (size_t)lds * 2 * sizeof(float4);
   // the single Perlin texture's tables in LDS behind the whole preorder, when they fit (scene 7: 158 KiB
   // of preorder + 4.75 KiB of tables in 160 KiB)
   d->gen_perlin_lds = -1;
-  if ((big || big4) && cfg.gen_perlin && s->n_perlins == 1 && lds_bytes + kPerlinLdsBytes <= (size_t)prop.sharedMemPerBlock) {
+  if (big && cfg.gen_perlin && s->n_perlins == 1 && lds_bytes + kPerlinLdsBytes <= (size_t)prop.sharedMemPerBlock) {
     d->gen_perlin_lds = (int32_t)lds_bytes;
     lds_bytes += kPerlinLdsBytes;
   }
   d->gen_lds_bytes = lds_bytes;
-  const void *fn = big4 ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, 1024>
-                              : (const void *)rt_general_kernel<kFeatAll, true, 1024>)
-                 : big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
+  const void *fn = big ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true, kBigBlock>
                              : (const void *)rt_general_kernel<kFeatAll, true, kBigBlock>)
                  : batch ? (fb ? (const void *)rt_general_kernel<kFeatBook1, true> : (const void *)rt_general_kernel<kFeatAll, true>)
                          : (fb ? (const void *)rt_general_kernel<kFeatBook1> : (const void *)rt_general_kernel<kFeatAll>);
@@ -1387,9 +1153,6 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->ch_arena) (void)hipFree(d->ch_arena);
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
   if (d->status) (void)hipFree(d->status);
-  if (d->wave_stream) (void)hipStreamDestroy(d->wave_stream);
-  if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
-  if (d->ev_join) (void)hipEventDestroy(d->ev_join);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
   for (hipEvent_t e : d->ev_main)
     if (e) (void)hipEventDestroy(e);
@@ -1403,54 +1166,18 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.cost_out = d->lpt_cost;
   P.draw_out = d->draw_out;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
-  P.sample_cost = (uint32_t)d->cfg.sample_cost;
-  P.order = nullptr;
   P.n_coop = nullptr;
-  // at the chain kernel's occupancy (4: no spills) on its grid, else the lane kernel's
-  if (d->cfg.chain_occ == 4) {
-    const dim3 g4((unsigned)d->chain_grid), blk(b1::kBlock);
-    if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true, 4>), g4, blk, d->b1_lds_bytes, st, P, d_out);
-    else hipLaunchKernelGGL((rt_book1_cost_kernel<false, 4>), g4, blk, 0, st, P, d_out);
-    return;
-  }
-  const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-  if (d->b1_lds_bytes)
-    hipLaunchKernelGGL((rt_book1_cost_kernel<true>), g1, blk, d->b1_lds_bytes, st, P, d_out);
-  else
-    hipLaunchKernelGGL((rt_book1_cost_kernel<false>), g1, blk, 0, st, P, d_out);
+  // at the chain kernel's occupancy, on its grid
+  const dim3 g((unsigned)d->chain_grid), blk(b1::kBlock);
+  if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true>), g, blk, d->b1_lds_bytes, st, P, d_out);
+  else hipLaunchKernelGGL((rt_book1_cost_kernel<false>), g, blk, 0, st, P, d_out);
 }
 
-static void launch_wave_kernel(rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st, int mode,
-                               int lane_grid) {
-  (void)hipEventRecord(d->ev_fork, st);
-  (void)hipStreamWaitEvent(d->wave_stream, d->ev_fork, 0);
-  // as many workgroups as the plan may give it; the lane kernel leaves it that many CU slots
-  const dim3 gw((unsigned)(lane_grid / 2 > 0 ? lane_grid / 2 : 1)), blk(b1::kBlock);
-  const bool lds = d->b1_lds_bytes != 0;
-  if (mode == 2) {
-    if (lds) hipLaunchKernelGGL((rt_book1_wave_kernel<true, 2>), gw, blk, d->b1_lds_bytes, d->wave_stream, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_wave_kernel<false, 2>), gw, blk, 0, d->wave_stream, V, d_out);
-  } else {
-    if (lds) hipLaunchKernelGGL((rt_book1_wave_kernel<true, 0>), gw, blk, d->b1_lds_bytes, d->wave_stream, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_wave_kernel<false, 0>), gw, blk, 0, d->wave_stream, V, d_out);
-  }
-}
-
-// The chain kernel's variants: LDS / global scene, and its occupancy target (launch bounds)
-static const void *chain_kernel_fn(bool lds, int occ) {
-  if (occ == 4) return lds ? (const void *)rt_book1_chain_kernel<true, 4> : (const void *)rt_book1_chain_kernel<false, 4>;
-  return lds ? (const void *)rt_book1_chain_kernel<true, 5> : (const void *)rt_book1_chain_kernel<false, 5>;
-}
 static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
   const size_t lds = d->b1_lds_bytes, bytes = lds + b1::kHandoffBytes;  // (+ the intra-wave cut handoff)
-  if (d->cfg.chain_occ == 4) {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 4>), gc, blk, bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 4>), gc, blk, bytes, st, V, d_out);
-  } else {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 5>), gc, blk, bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 5>), gc, blk, bytes, st, V, d_out);
-  }
+  if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, bytes, st, V, d_out);
+  else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, bytes, st, V, d_out);
 }
 
 // Records of a chain launch: grown on demand, up to the RT_CHAIN_MB budget (the planner keeps
@@ -1488,11 +1215,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   ChainModel m;
   m.ratio = (float)V.S.cam.spp / (float)cfg.lpt_spp;
   m.grid_waves = d->chain_grid * (b1::kBlock / 64);
-  m.lat = cfg.lane_lat;
-  m.thr = cfg.lane_thr;
-  m.coop = cfg.lane_coop;
+  m.lat = kLaneLat;
+  m.thr = kLaneThr;
+  m.coop = kCoopStep;
   m.beta = cfg.chain_beta;
-  m.floor_beta = cfg.chain_floor;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
   m.width = V.S.cam.width;
@@ -1518,8 +1244,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
                      d->ch_wave_key);
-  if (cfg.coop_sort)
-    hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
+  hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
   hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, end, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
   if (cfg.debug) {  // diagnostic: synchronous peek at the plan
@@ -1530,7 +1255,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
             "c* %.1f c*_w %.1f\n", (long long)npix, c[kCnItems], c[kCnSplit], *(unsigned long long *)&c[kCnRec], d->ch_rec_cap, c[kCnWave],
             c[kCnCoopWaves], bits_as_float(c[kCnCstar]), bits_as_float(c[kCnCstarW]));
   }
-  V.order = nullptr;
   V.ch_px = d->ch_px;
   V.ch_items = d->ch_items;
   V.ch_n_items = d->ch_cnt + kCnItems;
@@ -1665,62 +1389,16 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   return 0;
 }
 
-// Lane or group launch: longest-first order from the pre-pass, the heaviest pixels on whole waves.
-static int launch_lane(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix,
-                       bool use_group) {
-  const Config &cfg = d->cfg;
+// Lane launch (low spp, small launches, RT_MODE=lane): pixels in row order, one per lane.
+static int launch_lane(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st) {
   const bool lds = d->b1_lds_bytes != 0;
-  if (cfg.lpt && V.S.cam.spp >= 4 * cfg.lpt_spp && npix >= 4096) {
-    launch_cost_pass(d, V, d_out, st);
-    HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
-    unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);  // after the 516 counters
-    const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
-    hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
-    const int64_t thr = (int64_t)cfg.coop_steps * cfg.lpt_spp;
-    const int coop_bucket = cfg.coop_steps < 0 ? -1 : (thr < (int64_t)UINT32_MAX ? (int)lpt_bucket((uint32_t)thr) : 255);
-    LptModel model;
-    model.spp_ratio = (float)V.S.cam.spp / (float)cfg.lpt_spp;
-    model.grid_waves = (use_group ? d->g_grid : d->b1_grid) * (b1::kBlock / 64);
-    model.lat_step = use_group ? cfg.group_lat : cfg.lane_lat;
-    model.thr_step = use_group ? cfg.group_thr : cfg.lane_thr;
-    model.coop_step = use_group ? cfg.group_coop : cfg.lane_coop;
-    model.lanes_per_wave = use_group ? 64 / grp::kG : 64;
-    const int coop_waves = lds ? cfg.coop_waves : 0;
-    hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, coop_bucket, coop_waves, model);
-    hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
-    if (coop_waves != 0 && cfg.coop_sort)
-      hipLaunchKernelGGL(lpt_coop_sort_kernel, dim3(1), dim3(1024), 0, st, d->lpt_cost, d->lpt_hist, d->lpt_order);
-    HIP_OK(hipGetLastError());
-    V.order = d->lpt_order;
-    if (coop_waves != 0) {
-      V.n_coop = d->lpt_hist + 512;
-      V.coop_counter = (int32_t *)(d->lpt_hist + 513);
-      V.coop_waves_dev = d->lpt_hist + 515;
-    }
-  }
+  V.n_coop = nullptr;
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
-  const bool waves = V.n_coop != nullptr;
-  if (waves) launch_wave_kernel(d, V, d_out, st, 0, use_group ? d->g_grid : d->b1_grid);
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
-  if (use_group) {  // eight lanes per pixel (rt_group.h)
-    const dim3 gg((unsigned)d->g_grid), gb(grp::kBlock);
-    if (lds) hipLaunchKernelGGL((rt_book1_group_kernel<true>), gg, gb, d->g_lds_bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_group_kernel<false>), gg, gb, d->g_lds_bytes, st, V, d_out);
-  } else {
-    const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
-    if (cfg.lane_occ == 4) {
-      if (lds) hipLaunchKernelGGL((rt_book1_kernel<true, 4>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-      else hipLaunchKernelGGL((rt_book1_kernel<false, 4>), g1, blk, 0, st, V, d_out);
-    } else {
-      if (lds) hipLaunchKernelGGL((rt_book1_kernel<true, 5>), g1, blk, d->b1_lds_bytes, st, V, d_out);
-      else hipLaunchKernelGGL((rt_book1_kernel<false, 5>), g1, blk, 0, st, V, d_out);
-    }
-  }
+  const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
+  if (lds) hipLaunchKernelGGL((rt_book1_kernel<true>), g1, blk, d->b1_lds_bytes, st, V, d_out);
+  else hipLaunchKernelGGL((rt_book1_kernel<false>), g1, blk, 0, st, V, d_out);
   HIP_OK(hipGetLastError());
-  if (waves) {
-    HIP_OK(hipEventRecord(d->ev_join, d->wave_stream));
-    HIP_OK(hipStreamWaitEvent(st, d->ev_join, 0));
-  }
   if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
   return 0;
 }
@@ -1734,12 +1412,6 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.n_lds = d->gen_lds;
   V.perlin_lds = d->gen_perlin_lds;
   const size_t lds_bytes = d->gen_lds_bytes;
-  if (V.batch && d->gen_block == 1024) {
-    const dim3 bb(1024);
-    if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, 1024>), g, bb, lds_bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_general_kernel<kFeatBook1, true, 1024>), g, bb, lds_bytes, st, V, d_out);
-    return;
-  }
   if (V.batch && d->gen_block == kBigBlock) {
     const dim3 bb(kBigBlock);
     if (all) hipLaunchKernelGGL((rt_general_kernel<kFeatAll, true, kBigBlock>), g, bb, lds_bytes, st, V, d_out);
@@ -1763,7 +1435,6 @@ static int pick_mode(const rt_device_scene *d, int64_t npix) {
   const bool chain_ok = cfg.lpt && spp >= 4 * cfg.lpt_spp && spp >= 2 * cfg.chain_min_seg && npix >= 4096 &&
                         d->view.cam.max_depth >= 1;
   if (cfg.mode == kModeChain) return chain_ok ? kModeChain : kModeLane;
-  if (cfg.mode == kModeGroup) return d->g_grid > 0 ? kModeGroup : kModeLane;
   if (cfg.mode == kModeLane) return kModeLane;
   // auto: the chain render whenever it applies (measured ahead of the lane kernel at every N, from
   // 1.16x at N = 1 to 2.2x at N = 8: DESIGN.md §5); the lane kernel for low spp / small launches
@@ -1780,7 +1451,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     V.n_rows = n_rows;
     const int mode = pick_mode(d, npix);
     if (mode == kModeChain) return launch_chain(d, V, d_out, st, npix);
-    return launch_lane(d, V, d_out, st, npix, mode == kModeGroup);
+    return launch_lane(d, V, d_out, st);
   }
   if (d->general) {
     const Config &cfg = d->cfg;
@@ -1805,14 +1476,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
-      LptModel model;
-      model.spp_ratio = 1.0f;
-      model.grid_waves = d->gen_grid * (d->gen_block / 64);
-      model.lat_step = kLaneLat;
-      model.thr_step = kLaneThr;
-      model.coop_step = kCoopStep;
-      model.lanes_per_wave = 64;
-      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist, sums, 255, 0, model);
+      hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist);
       hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
       HIP_OK(hipGetLastError());
       G.order = d->lpt_order;
@@ -2025,22 +1689,6 @@ extern "C" int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t se
   return 0;
 }
 
-extern "C" int rt_scene_px_time(rt_device_scene *d, uint32_t *times, uint32_t *cost, int32_t *order,
-                                uint32_t *n_coop, int64_t n) {
-  if (!d || !d->book1) return rt_set_error("rt_scene_px_time: not a Book-1 scene"), -1;
-  if (n < 0 || n > (int64_t)d->width * d->height) return rt_set_error("rt_scene_px_time: bad count"), -1;
-  HIP_OK(hipSetDevice(d->device));
-  HIP_OK(hipDeviceSynchronize());
-  if (times) {
-    if (!d->px_time) return rt_set_error("rt_scene_px_time: upload with RT_PX_TIME=1"), -1;
-    HIP_OK(hipMemcpy(times, d->px_time, (size_t)n * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  }
-  if (cost) HIP_OK(hipMemcpy(cost, d->lpt_cost, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (order) HIP_OK(hipMemcpy(order, d->lpt_order, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (n_coop) HIP_OK(hipMemcpy(n_coop, d->lpt_hist + 512, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  return 0;
-}
-
 // Diagnostics of the last chain launch (RT_PX_TIME=1 at upload): one row of 16 u32 per work item, in
 // item order -- pixel, segment, K, whole-wave (1) or lane (0), start, end (wall_clock64 ticks, low 32
 // bits), records (samples for segment 0 / unsplit), end flags (bit 0 linked, bit 1 ended), link
@@ -2120,15 +1768,13 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   if (!d->book1) {
     snprintf(buf, sizeof buf, "%s<%d%s>", d->general ? "rt_general_kernel" : "rt_render_rows_kernel",
              (d->features & ~kFeatBook1) == 0 ? (int)kFeatBook1 : (int)kFeatAll,
-             d->general && d->gen_block == 1024 ? ", true, 1024" : d->general && d->gen_block == kBigBlock ? ", true, 768"
+             d->general && d->gen_block == kBigBlock ? ", true, 768"
              : d->general && d->view.pre && d->cfg.gen_batch ? ", true" : d->general ? ", false" : "");
     return buf;
   }
   const int mode = pick_mode(d, (int64_t)d->width * d->height);
   const char *lds = d->b1_lds_bytes ? "true" : "false";
-  if (mode == kModeChain) snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %d>", lds, d->cfg.chain_occ);
-  else if (mode == kModeGroup) snprintf(buf, sizeof buf, "rt_book1_group_kernel<%s>", lds);
-  else snprintf(buf, sizeof buf, "rt_book1_kernel<%s, %d>", lds, d->cfg.lane_occ);
+  snprintf(buf, sizeof buf, "%s<%s>", mode == kModeChain ? "rt_book1_chain_kernel" : "rt_book1_kernel", lds);
   return buf;
 }
 

@@ -69,8 +69,7 @@ def test_gpu_api_world_matches_reference_build(wid, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"RT_MODE": "lane"}, {"RT_MODE": "group"}, {"RT_MODE": "chain", "RT_LPT_SPP": "2"},
-                                 {"RT_BOOK1": "0"}])
+@pytest.mark.parametrize("env", [{"RT_MODE": "lane"}, {"RT_MODE": "chain", "RT_LPT_SPP": "2"}, {"RT_BOOK1": "0"}])
 @pytest.mark.parametrize("wid", BOOK1)
 def test_gpu_api_world_book1_variants(wid, env, tmp_path):
     ref, e = golden(wid)

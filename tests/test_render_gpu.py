@@ -211,12 +211,7 @@ CHAIN = {"RT_MODE": "chain", "RT_LPT_SPP": "1", "RT_CHAIN_MIN_SEG": "4"}
 
 @pytest.mark.parametrize("env", [
     {}, {"RT_BOOK1": "0"}, {"RT_BOOK1": "0", "RT_GENERAL": "0"}, {"RT_BOOK1_LDS": "0"},
-    {"RT_MODE": "lane"}, {"RT_MODE": "lane", "RT_LPT": "0"}, {"RT_MODE": "lane", "RT_LPT_SPP": "1"},
-    {"RT_MODE": "lane", "RT_COOP_STEPS": "50"}, {"RT_MODE": "lane", "RT_COOP_WAVES": "0"},
-    {"RT_MODE": "lane", "RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024"},
-    {"RT_MODE": "lane", "RT_LPT_SPP": "1", "RT_COOP_STEPS": "0", "RT_COOP_WAVES": "1024", "RT_BF": "0"},
-    {"RT_MODE": "lane", "RT_BOOK1_LDS": "0", "RT_LPT_SPP": "1"},
-    {"RT_MODE": "group"}, {"RT_MODE": "group", "RT_BOOK1_LDS": "0"}, {"RT_MODE": "group", "RT_LPT": "0"},
+    {"RT_MODE": "lane"}, {"RT_MODE": "lane", "RT_BOOK1_LDS": "0"},
     {"RT_SHADE_BATCH": "1"}, {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"},
     CHAIN,                                                         # the chain render, planned
     {**CHAIN, "RT_CHAIN_BETA": "0.001"},                           # every pixel split as far as allowed
