@@ -743,11 +743,17 @@ RT_D float perlin_noise_lds(const PerlinLds &P, f3 p) {  // src/texture.c:78-103
   return value;
 }
 
-// pl: perlins[0]'s LDS copy (pl.perm null: none)
-RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p, PerlinLds pl = PerlinLds{nullptr, nullptr}) {
+// pl: perlins[0]'s LDS copy (pl.perm null: none).  solid (optional): the solid texture the value
+// came from (its colour, as is), -1 otherwise.
+RT_D f3 texture_value(const DScene &S, int32_t tex, float u, float v, f3 p, PerlinLds pl = PerlinLds{nullptr, nullptr},
+                      int32_t *solid = nullptr) {
+  if (solid) *solid = -1;
   for (int hops = 0; hops < 16; hops++) {
     const rt_texture &t = S.textures[tex];
-    if (t.kind == RT_TEX_SOLID) return ld3(t.color);
+    if (t.kind == RT_TEX_SOLID) {
+      if (solid) *solid = tex;
+      return ld3(t.color);
+    }
     if (t.kind == RT_TEX_CHECKER) {  // src/texture.c:12-22
       const int iu = (int)floorf(u / t.scale);
       const int iv = (int)floorf(v / t.scale);
@@ -806,9 +812,11 @@ RT_D f3 emit(const DScene &S, const Rec &r, PerlinLds pl = PerlinLds{nullptr, nu
 }
 
 // Material_scatter (src/material.c:103-120).  Returns false when the path ends at this hit.
+// solid (optional): the solid texture the albedo is the colour of, kUnitAlbedo for (1, 1, 1), else -1.
+constexpr int32_t kUnitAlbedo = -2;
 template <int F>
 RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 &albedo, bool &skip_pdf,
-                  PerlinLds pl = PerlinLds{nullptr, nullptr}) {
+                  PerlinLds pl = PerlinLds{nullptr, nullptr}, int32_t *solid = nullptr) {
   const rt_material &m = S.materials[r.material];
   switch (m.tag) {
   case RT_MAT_LAMBERTIAN: {  // src/material.c:23-37
@@ -820,14 +828,14 @@ RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 
     rtm::sincosf(phi, &sphi, &cphi);
     const float sq = sqrtf(r2);
     out = onb_local(b, mk(cphi * sq, sphi * sq, sqrtf(1.0f - r2)));
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl, solid);
     skip_pdf = false;
     return true;
   }
   case RT_MAT_METAL: {  // src/material.c:48-58
     const f3 refl = reflect(normalize(r_in), r.normal);
     out = add(refl, scale(rand_unit_vector(g), m.param));
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl, solid);
     skip_pdf = true;
     if (dot(out, r.normal) < 0.0f) out = refl;
     return true;
@@ -849,12 +857,13 @@ RT_D bool scatter(const DScene &S, const Rec &r, f3 r_in, Pcg32 &g, f3 &out, f3 
       out = add(perp, para);
     }
     albedo = mk(1.0f, 1.0f, 1.0f);
+    if (solid) *solid = kUnitAlbedo;
     skip_pdf = true;
     return true;
   }
   case RT_MAT_ISOTROPIC: {  // src/material.c:93-98
     out = rand_unit_vector(g);
-    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl);
+    albedo = texture_value(S, m.texture, r.u, r.v, r.p, pl, solid);
     skip_pdf = false;
     return true;
   }

@@ -28,7 +28,51 @@ struct GeneralView {
                              // flat - 1 box entries in the same step (RT_GEN_FLAT; 0: branched dispatch)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
   int32_t perlin_lds;        // kAllLds: byte offset of perlins[0]'s LDS copy (PerlinLds) behind the preorder; -1: none
+  float4 *xrec;              // explicit path records: kMaxDepth per thread of the grid, thread-contiguous
+  int32_t code_bits;         // 4 (scenes of <= 13 textures) or 8: width of a path record's albedo code
 };
+
+// Path records as runs of albedo codes in one u64 register pair (PathRuns).  A record's albedo is a
+// b-bit code (b = code_bits): 1..2^b - 3 = the colour of solid texture code - 1, 2^b - 2 = (1, 1, 1),
+// 2^b - 1 = explicit: the record (albedo, pdf weight or 1) is in the thread's xrec slot -- image /
+// noise textures, weighted bounces, textures past the code range.  Consecutive bounces of one code
+// (a random walk in a medium: scene 7's subsurface sphere runs every such path to max_depth) are one
+// run of (code, length - 1: 6 bits); bits 60..63 count the runs, 15 = full: the bounces past the
+// runs are explicit.  The fold reads back the same floats.
+struct PathRuns {
+  uint64_t w;
+  int cb, run_bits, max_runs;
+  uint32_t code_explicit;
+};
+RT_D PathRuns runs_init(int code_bits) {
+  PathRuns R;
+  R.w = 0;
+  R.cb = code_bits;
+  R.run_bits = code_bits + 6;
+  R.max_runs = 60 / R.run_bits;
+  R.code_explicit = (1u << code_bits) - 1u;
+  return R;
+}
+// Record bounce `code`; false when it is past the runs (store it explicitly).
+RT_D bool runs_push(PathRuns &R, uint32_t code) {
+  const uint32_t cnt = (uint32_t)(R.w >> 60);
+  if (cnt == 15u) return false;
+  if (cnt > 0u) {
+    const int at = R.run_bits * (int)(cnt - 1u);
+    const uint32_t last = (uint32_t)(R.w >> at) & R.code_explicit;
+    if (last == code) {  // (length - 1 <= 63: at most kMaxDepth bounces)
+      R.w += 1ull << (at + R.cb);
+      return true;
+    }
+  }
+  if ((int)cnt < R.max_runs) {
+    R.w |= (uint64_t)code << (R.run_bits * (int)cnt);
+    R.w += 1ull << 60;
+    return true;
+  }
+  R.w |= 15ull << 60;
+  return false;
+}
 
 // -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
 enum {
@@ -39,7 +83,7 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsRecords, kGsExplicit, kGsN
 };
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
@@ -383,10 +427,12 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   // per-lane path state (path_color's locals, kept across iterations).  A recorded bounce's
   // emission is always +0 (only SurfaceNormal and DiffuseLight emit, and neither scatters:
   // src/material.c:103-142), so the record is (albedo, pdf weight) and the fold adds +0 as the
-  // reference's vec3_add(emission_color, scatter_color) does.
-  f3 rec_a[kMaxDepth];
-  float rec_w[kFull ? kMaxDepth : 1];
-  uint64_t weighted = 0;
+  // reference's vec3_add(emission_color, scatter_color) does.  Records: albedo codes (kCode*) in
+  // registers, explicit ones in the thread's xrec slots (thread-contiguous: a lane's records share
+  // cache lines, where private arrays interleave every dword across the wave's lanes).
+  PathRuns runs = runs_init(V.code_bits);
+  const uint32_t code_explicit = runs.code_explicit, code_unit = code_explicit - 1u;
+  float4 *const xrec = V.xrec + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * kMaxDepth;
   int n = 0, depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
   uint32_t rays = 0;
@@ -546,7 +592,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
       depth = S.cam.max_depth;
       n = 0;
-      weighted = 0;
+      runs.w = 0;
       need_sample = false;
     }
     GS_ADD(kGsCycCamera, GS_NOW() - gs_c);
@@ -607,7 +653,8 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         GS_ADD(kGsPassPerlin, gs_perlin);
 #endif
         gs_c = GS_NOW();
-        const bool scattered = scatter<F>(S, r, d, g, dir, albedo, skip_pdf, pl);
+        int32_t solid = -1;
+        const bool scattered = scatter<F>(S, r, d, g, dir, albedo, skip_pdf, pl, &solid);
 #ifdef RT_GEN_STATS
         GS_ADD(gs_perlin ? kGsCycScatterPerlin : kGsCycScatter, GS_NOW() - gs_c);
 #endif
@@ -615,18 +662,24 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           tail = e;
           path_done = true;
         } else {
-          rec_a[n] = albedo;
+          uint32_t code = solid == kUnitAlbedo ? code_unit
+                          : (solid >= 0 && (uint32_t)solid + 1u < code_unit ? (uint32_t)solid + 1u : code_explicit);
+          float w = 1.0f;  // (x * 1.0f == x: the unweighted record's fold step is unchanged)
           if (kFull) {
             if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
               gs_c = GS_NOW();
               if (g.f32() < prob) dir = lights_rand(S, r.p, g);
               const float sp = scatter_pdf(S, r.material, r.normal, dir);
               const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, dir);
-              rec_w[n] = sp / spdf;
-              weighted |= 1ull << n;
+              w = sp / spdf;
+              code = code_explicit;
               GS_ADD(kGsCycLights, GS_NOW() - gs_c);
             }
           }
+          if (!runs_push(runs, code)) code = code_explicit;
+          if (code == code_explicit) xrec[n] = make_float4(albedo.x, albedo.y, albedo.z, w);
+          GS_ADD(kGsRecords, 1);  // (per lane: summed over every lane at the end)
+          GS_ADD(kGsExplicit, code == code_explicit);
           n++;
           o = r.p;
           d = dir;
@@ -645,10 +698,36 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     if (!write) {
     // ---- fold innermost-first, accumulate, next sample / pixel (src/raytracing.c:124-131)
     f3 c = tail;
-    for (int k = n - 1; k >= 0; k--) {
-      f3 x = mul(rec_a[k], c);
-      if (kFull && ((weighted >> k) & 1)) x = scale(x, rec_w[k]);
-      c = add(mk(0.0f, 0.0f, 0.0f), x);
+    {
+      const uint32_t cnt = (uint32_t)(runs.w >> 60);
+      const int nr = cnt == 15u ? runs.max_runs : (int)cnt;
+      int covered = 0;  // bounces in the runs; those past them are explicit
+      for (int r = 0; r < nr; r++) covered += (int)((runs.w >> (runs.run_bits * r + runs.cb)) & 63u) + 1;
+      int k = n - 1;
+      int r = nr - 1, left = 0;  // the run bounce k is in, and its bounces not yet folded
+      uint32_t code = code_explicit;
+      f3 a = mk(1.0f, 1.0f, 1.0f);
+      for (; k >= 0; k--) {
+        if (k < covered) {
+          if (left == 0) {  // enter the next run down
+            code = (uint32_t)(runs.w >> (runs.run_bits * r)) & code_explicit;
+            left = (int)((runs.w >> (runs.run_bits * r + runs.cb)) & 63u) + 1;
+            r--;
+            if (code != code_explicit) a = code == code_unit ? mk(1.0f, 1.0f, 1.0f) : ld3(S.textures[code - 1].color);
+          }
+          left--;
+        } else {
+          code = code_explicit;
+        }
+        f3 x;
+        if (code == code_explicit) {
+          const float4 e = xrec[k];
+          x = scale(mul(mk(e.x, e.y, e.z), c), e.w);
+        } else {
+          x = mul(a, c);
+        }
+        c = add(mk(0.0f, 0.0f, 0.0f), x);
+      }
     }
     acc = add(acc, c);
     s++;
@@ -673,8 +752,9 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     GS_ADD(kGsCycWrite, GS_NOW() - gs_c);
   }
 #ifdef RT_GEN_STATS
-  if (V.stats && lane == 0)
-    for (int q = 0; q < kGsN; q++) atomicAdd(V.stats + q, gs[q]);
+  if (V.stats)
+    for (int q = 0; q < kGsN; q++)
+      if (lane == 0 || q == kGsRecords || q == kGsExplicit) atomicAdd(V.stats + q, gs[q]);
 #endif
 #undef GS_NOW
 #undef GS_ADD

@@ -663,6 +663,7 @@ struct rt_device_scene {
   void *gen_arena = nullptr;
   int32_t *gen_counter = nullptr;
   int gen_grid = 0, gen_block = 256;
+  float4 *gen_xrec = nullptr;  // explicit path records of the general kernel (rt_general.h: GeneralView.xrec)
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_lds = 0;
   size_t gen_lds_bytes = 0;   // dynamic LDS of the general kernel
@@ -1035,6 +1036,8 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, d->gen_block, lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->gen_grid = prop.multiProcessorCount * per_cu;
+  // explicit path records (rt_general.h: kCodeExplicit), kMaxDepth per thread of the grid
+  HIP_OK(hipMalloc(&d->gen_xrec, (size_t)d->gen_grid * d->gen_block * kMaxDepth * sizeof(float4)));
   d->general = true;
   if (cfg.debug)
     fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, perlin in lds %d, "
@@ -1145,6 +1148,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   (void)hipFree(d->arena);
   if (d->b1_arena) (void)hipFree(d->b1_arena);
   if (d->gen_arena) (void)hipFree(d->gen_arena);
+  if (d->gen_xrec) (void)hipFree(d->gen_xrec);
   if (d->px_time) (void)hipFree(d->px_time);
   if (d->seg_time) (void)hipFree(d->seg_time);
   if (d->mig_q) (void)hipFree(d->mig_q);
@@ -1464,6 +1468,8 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     G.order = nullptr;
     G.cost_out = nullptr;
     G.stats = nullptr;
+    G.xrec = d->gen_xrec;
+    G.code_bits = d->view.n_textures <= 13 ? 4 : 8;
     const bool all = (d->features & ~kFeatBook1) != 0;
     const dim3 gg((unsigned)d->gen_grid), gb(gen::kBlock);
     if (cfg.lpt && G.S.cam.spp >= 4 * cfg.lpt_spp && npix >= 4096) {  // longest-first order (rays per pixel)
@@ -1502,7 +1508,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
           "kind_other", "cyc_record", "cyc_emit", "cyc_scatter", "cyc_lights", "cyc_fold", "mat_lam", "mat_metal",
           "mat_diel", "mat_iso", "mat_end", "tex_solid", "tex_checker", "tex_image", "tex_perlin",
           "cyc_scatter_perlin", "pass_perlin", "miss", "cyc_camera", "cyc_begin", "cyc_top", "cyc_classify",
-          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write"};
+          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write", "records", "explicit"};
       fprintf(stderr, "[rtc] gen stats:");
       for (int k = 0; k < gen::kGsN; k++) fprintf(stderr, " %s=%llu", names[k], q[k]);
       fprintf(stderr, "\n");

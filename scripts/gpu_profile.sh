@@ -26,7 +26,7 @@ ap = argparse.ArgumentParser(); ap.add_argument("--scene", type=int, default=1);
 ap.add_argument("--spp", type=int, default=1000); ap.add_argument("--depth", type=int, default=50)
 a, _ = ap.parse_known_args()
 import rtc
-s = rtc.Scene.preset(a.scene, a.width, 1, 1)
+s = rtc.Scene.preset(a.scene, a.width, 1, 1, substitute_earth=True)
 print(f"s{a.scene}_{s.width}x{s.height}_{a.spp}spp_d{a.depth}_n1", s.width * s.height * a.spp, rtc.build_id())
 PY
 )
