@@ -28,40 +28,43 @@ struct GeneralView {
                              // flat - 1 box entries in the same step (RT_GEN_FLAT; 0: branched dispatch)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
   int32_t perlin_lds;        // kAllLds: byte offset of perlins[0]'s LDS copy (PerlinLds) behind the preorder; -1: none
-  float4 *xrec;              // explicit path records: kMaxDepth per thread of the grid, thread-contiguous
+  float4 *xrec;              // explicit albedos of path records: kMaxDepth per thread of the grid, thread-contiguous
+  float *xw;                 // pdf weights of path records: kMaxDepth per thread of the grid, thread-contiguous
   int32_t code_bits;         // 4 (scenes of <= 13 textures) or 8: width of a path record's albedo code
 };
 
-// Path records as runs of albedo codes in one u64 register pair (PathRuns).  A record's albedo is a
-// b-bit code (b = code_bits): 1..2^b - 3 = the colour of solid texture code - 1, 2^b - 2 = (1, 1, 1),
-// 2^b - 1 = explicit: the record (albedo, pdf weight or 1) is in the thread's xrec slot -- image /
-// noise textures, weighted bounces, textures past the code range.  Consecutive bounces of one code
-// (a random walk in a medium: scene 7's subsurface sphere runs every such path to max_depth) are one
-// run of (code, length - 1: 6 bits); bits 60..63 count the runs, 15 = full: the bounces past the
-// runs are explicit.  The fold reads back the same floats.
+// Path records as runs of codes in one u64 register pair (PathRuns).  A record's code is its albedo
+// in b bits (b = code_bits) -- 1..2^b - 3 = the colour of solid texture code - 1, 2^b - 2 = (1, 1, 1),
+// 2^b - 1 = explicit: the albedo is in the thread's xrec slot (image / noise textures, textures past
+// the code range) -- and bit b: weighted, the pdf weight is in the thread's xw slot.  Consecutive
+// bounces of one code (a random walk in a medium: scene 7's subsurface sphere runs every such path
+// to max_depth) are one run of (code, length - 1: 6 bits); bits 60..63 count the runs, 15 = full:
+// the bounces past the runs are explicit and weighted (weight 1 when the bounce had none:
+// x * 1.0f == x).  The fold reads back the same floats.
 struct PathRuns {
   uint64_t w;
-  int cb, run_bits, max_runs;
-  uint32_t code_explicit;
+  int cb, code_bits, run_bits, max_runs;
+  uint32_t code_mask;
 };
-RT_D PathRuns runs_init(int code_bits) {
+RT_D PathRuns runs_init(int albedo_bits) {
   PathRuns R;
   R.w = 0;
-  R.cb = code_bits;
-  R.run_bits = code_bits + 6;
+  R.cb = albedo_bits;
+  R.code_bits = albedo_bits + 1;
+  R.run_bits = R.code_bits + 6;
   R.max_runs = 60 / R.run_bits;
-  R.code_explicit = (1u << code_bits) - 1u;
+  R.code_mask = (1u << R.code_bits) - 1u;
   return R;
 }
-// Record bounce `code`; false when it is past the runs (store it explicitly).
+// Record a bounce of this code; false when it is past the runs (store it explicitly, weighted).
 RT_D bool runs_push(PathRuns &R, uint32_t code) {
   const uint32_t cnt = (uint32_t)(R.w >> 60);
   if (cnt == 15u) return false;
   if (cnt > 0u) {
     const int at = R.run_bits * (int)(cnt - 1u);
-    const uint32_t last = (uint32_t)(R.w >> at) & R.code_explicit;
+    const uint32_t last = (uint32_t)(R.w >> at) & R.code_mask;
     if (last == code) {  // (length - 1 <= 63: at most kMaxDepth bounces)
-      R.w += 1ull << (at + R.cb);
+      R.w += 1ull << (at + R.code_bits);
       return true;
     }
   }
@@ -83,7 +86,7 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsRecords, kGsExplicit, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsRecords, kGsExplicit, kGsWeighted, kGsN
 };
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
@@ -431,8 +434,12 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   // registers, explicit ones in the thread's xrec slots (thread-contiguous: a lane's records share
   // cache lines, where private arrays interleave every dword across the wave's lanes).
   PathRuns runs = runs_init(V.code_bits);
-  const uint32_t code_explicit = runs.code_explicit, code_unit = code_explicit - 1u;
-  float4 *const xrec = V.xrec + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * kMaxDepth;
+  const uint32_t code_explicit = (1u << runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << runs.cb;
+  // (every store leaves L2 for the fabric, at least a 32-B sector each: weights are stored in pairs,
+  // one 8-B store per two bounces, the even bounce's weight waiting in wpend)
+  const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
+  float wpend = 0.0f;
+  bool wprev = false;  // the previous (even) bounce was weighted: its weight is in wpend
   int n = 0, depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
   uint32_t rays = 0;
@@ -664,7 +671,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
         } else {
           uint32_t code = solid == kUnitAlbedo ? code_unit
                           : (solid >= 0 && (uint32_t)solid + 1u < code_unit ? (uint32_t)solid + 1u : code_explicit);
-          float w = 1.0f;  // (x * 1.0f == x: the unweighted record's fold step is unchanged)
+          float w = 1.0f;
           if (kFull) {
             if ((F & RT_FEAT_LIGHTS) && (S.features & RT_FEAT_LIGHTS) && !skip_pdf) {
               gs_c = GS_NOW();
@@ -672,14 +679,22 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
               const float sp = scatter_pdf(S, r.material, r.normal, dir);
               const float spdf = (1.0f - prob) * sp + prob * lights_pdf(S, r.p, dir);
               w = sp / spdf;
-              code = code_explicit;
+              code |= code_weighted;
               GS_ADD(kGsCycLights, GS_NOW() - gs_c);
             }
           }
-          if (!runs_push(runs, code)) code = code_explicit;
-          if (code == code_explicit) xrec[n] = make_float4(albedo.x, albedo.y, albedo.z, w);
+          if (!runs_push(runs, code)) code = code_explicit | code_weighted;
+          if ((code & code_explicit) == code_explicit) V.xrec[rec0 + n] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
+          const bool wt = (code & code_weighted) != 0;
+          if ((n & 1) == 0) {
+            wpend = w;
+            wprev = wt;
+          } else if (wt || wprev) {
+            *(float2 *)(V.xw + rec0 + n - 1) = make_float2(wpend, w);
+          }
           GS_ADD(kGsRecords, 1);  // (per lane: summed over every lane at the end)
-          GS_ADD(kGsExplicit, code == code_explicit);
+          GS_ADD(kGsExplicit, (code & code_explicit) == code_explicit);
+          GS_ADD(kGsWeighted, (code & code_weighted) != 0);
           n++;
           o = r.p;
           d = dir;
@@ -701,31 +716,28 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     {
       const uint32_t cnt = (uint32_t)(runs.w >> 60);
       const int nr = cnt == 15u ? runs.max_runs : (int)cnt;
-      int covered = 0;  // bounces in the runs; those past them are explicit
-      for (int r = 0; r < nr; r++) covered += (int)((runs.w >> (runs.run_bits * r + runs.cb)) & 63u) + 1;
-      int k = n - 1;
+      int covered = 0;  // bounces in the runs; those past them are explicit and weighted
+      for (int r = 0; r < nr; r++) covered += (int)((runs.w >> (runs.run_bits * r + runs.code_bits)) & 63u) + 1;
       int r = nr - 1, left = 0;  // the run bounce k is in, and its bounces not yet folded
-      uint32_t code = code_explicit;
+      uint32_t code = code_explicit | code_weighted;
       f3 a = mk(1.0f, 1.0f, 1.0f);
-      for (; k >= 0; k--) {
+      for (int k = n - 1; k >= 0; k--) {
         if (k < covered) {
           if (left == 0) {  // enter the next run down
-            code = (uint32_t)(runs.w >> (runs.run_bits * r)) & code_explicit;
-            left = (int)((runs.w >> (runs.run_bits * r + runs.cb)) & 63u) + 1;
+            code = (uint32_t)(runs.w >> (runs.run_bits * r)) & runs.code_mask;
+            left = (int)((runs.w >> (runs.run_bits * r + runs.code_bits)) & 63u) + 1;
             r--;
-            if (code != code_explicit) a = code == code_unit ? mk(1.0f, 1.0f, 1.0f) : ld3(S.textures[code - 1].color);
+            const uint32_t ca = code & code_explicit;
+            if (ca != code_explicit) a = ca == code_unit ? mk(1.0f, 1.0f, 1.0f) : ld3(S.textures[ca - 1].color);
           }
           left--;
-        } else {
-          code = code_explicit;
         }
-        f3 x;
-        if (code == code_explicit) {
-          const float4 e = xrec[k];
-          x = scale(mul(mk(e.x, e.y, e.z), c), e.w);
-        } else {
-          x = mul(a, c);
+        if ((code & code_explicit) == code_explicit) {
+          const float4 e = V.xrec[rec0 + k];
+          a = mk(e.x, e.y, e.z);
         }
+        f3 x = mul(a, c);
+        if (code & code_weighted) x = scale(x, (k & 1) == 0 && k == n - 1 ? wpend : V.xw[rec0 + k]);
         c = add(mk(0.0f, 0.0f, 0.0f), x);
       }
     }
@@ -754,7 +766,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
 #ifdef RT_GEN_STATS
   if (V.stats)
     for (int q = 0; q < kGsN; q++)
-      if (lane == 0 || q == kGsRecords || q == kGsExplicit) atomicAdd(V.stats + q, gs[q]);
+      if (lane == 0 || q == kGsRecords || q == kGsExplicit || q == kGsWeighted) atomicAdd(V.stats + q, gs[q]);
 #endif
 #undef GS_NOW
 #undef GS_ADD

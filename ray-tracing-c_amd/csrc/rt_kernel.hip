@@ -663,7 +663,8 @@ struct rt_device_scene {
   void *gen_arena = nullptr;
   int32_t *gen_counter = nullptr;
   int gen_grid = 0, gen_block = 256;
-  float4 *gen_xrec = nullptr;  // explicit path records of the general kernel (rt_general.h: GeneralView.xrec)
+  float4 *gen_xrec = nullptr;  // explicit path records of the general kernel (rt_general.h: GeneralView.xrec / xw)
+  float *gen_xw = nullptr;
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_lds = 0;
   size_t gen_lds_bytes = 0;   // dynamic LDS of the general kernel
@@ -1036,8 +1037,10 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, d->gen_block, lds_bytes));
   if (per_cu < 1) per_cu = 1;
   d->gen_grid = prop.multiProcessorCount * per_cu;
-  // explicit path records (rt_general.h: kCodeExplicit), kMaxDepth per thread of the grid
-  HIP_OK(hipMalloc(&d->gen_xrec, (size_t)d->gen_grid * d->gen_block * kMaxDepth * sizeof(float4)));
+  // explicit path records (rt_general.h: PathRuns), kMaxDepth albedos and weights per thread of the grid
+  const size_t threads = (size_t)d->gen_grid * d->gen_block;
+  HIP_OK(hipMalloc(&d->gen_xrec, threads * kMaxDepth * (sizeof(float4) + sizeof(float))));
+  d->gen_xw = (float *)(d->gen_xrec + threads * kMaxDepth);
   d->general = true;
   if (cfg.debug)
     fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, perlin in lds %d, "
@@ -1469,6 +1472,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     G.cost_out = nullptr;
     G.stats = nullptr;
     G.xrec = d->gen_xrec;
+    G.xw = d->gen_xw;
     G.code_bits = d->view.n_textures <= 13 ? 4 : 8;
     const bool all = (d->features & ~kFeatBook1) != 0;
     const dim3 gg((unsigned)d->gen_grid), gb(gen::kBlock);
@@ -1508,7 +1512,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
           "kind_other", "cyc_record", "cyc_emit", "cyc_scatter", "cyc_lights", "cyc_fold", "mat_lam", "mat_metal",
           "mat_diel", "mat_iso", "mat_end", "tex_solid", "tex_checker", "tex_image", "tex_perlin",
           "cyc_scatter_perlin", "pass_perlin", "miss", "cyc_camera", "cyc_begin", "cyc_top", "cyc_classify",
-          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write", "records", "explicit"};
+          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write", "records", "explicit", "weighted"};
       fprintf(stderr, "[rtc] gen stats:");
       for (int k = 0; k < gen::kGsN; k++) fprintf(stderr, " %s=%llu", names[k], q[k]);
       fprintf(stderr, "\n");
