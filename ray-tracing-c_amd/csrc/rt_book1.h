@@ -332,10 +332,15 @@ RT_D void sphere_test_data(float4 s, int idx, Lane &L, float tmin) {
 // (skip = 1 + the node's subtree size in items).  The box test sees exactly the reference's t_max:
 // every item before p in preorder that the reference would test has been tested, in order.
 constexpr uint32_t kLeaf9 = 0x80000000u;
+// Items are stored as two arrays (q0 of every item, then q1 of every item: na = V.n_items9_alloc
+// apart): a ds_read_b128 lane group (16 lanes, one 256-B bank row) then spreads random items over 16
+// slots, where 32-B interleaved items use only 8 of them (more bank conflicts on the step's read).
+RT_D float4 it_q0(const float4 *items, uint32_t p) { return items[p]; }
+RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint32_t)na + p]; }
 
 RT_D bool trav_step_v9(const Book1View &V, const float4 *items, Lane &L, float tmin) {
   const uint32_t p = L.cur;
-  float4 q0 = items[2 * p], q1 = items[2 * p + 1];
+  float4 q0 = it_q0(items, p), q1 = it_q1(items, V.n_items9_alloc, p);
   // both halves in one LDS round trip: without this the compiler sinks the q1.xy / q1.z reads into
   // the branches that use them, i.e. three dependent round trips per step.  (Reading the successor
   // one step ahead measured slower: its moves and the re-read after a skip cost more than the latency.)
@@ -482,7 +487,7 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const CoopRay &C,
     float v0 = 0.0f, v1 = 0.0f;  // node: E, X; leaf: root
     uint32_t meta = 0;           // node: skip; leaf: index | kLeaf9
     if (q < n) {
-      const float4 q0 = items[2 * q], q1 = items[2 * q + 1];
+      const float4 q0 = it_q0(items, q), q1 = it_q1(items, V.n_items9_alloc, q);
       meta = __float_as_uint(q1.w);
       if (meta & kLeaf9) {
         v0 = coop_sphere_root(q0, C, tmin);
@@ -544,10 +549,10 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C
     if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
     const int n = k * 64 + lane;
     const bool live = n < V.n_bf_leaves;
-    const float4 h = items[2 * (live ? n : 0) + 1];
+    const float4 h = it_q1(items, V.n_items9_alloc, live ? n : 0);
     const uint32_t hw = __float_as_uint(h.w);
     const int pos = (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw);
-    const float r = coop_sphere_root(items[2 * pos], C, tmin);
+    const float r = coop_sphere_root(it_q0(items, pos), C, tmin);
     nan |= live && r != r;
     if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
   }
@@ -564,17 +569,17 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C
   return true;
 }
 
-RT_D bool bf_verify(const float4 *items, const CoopRay &C, float tmin, float best, int bp) {
+RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, float best, int bp) {
   const int lane = __lane_id();
   bool bad = false;
   for (int base = 0; base < bp; base += 64) {  // wave-uniform bound
     const int q = base + lane;
     if (q < bp) {
-      const float4 q1 = items[2 * q + 1];
+      const float4 q1 = it_q1(items, na, q);
       const uint32_t w = __float_as_uint(q1.w);
       if (!(w & kLeaf9) && (uint32_t)bp < (uint32_t)q + __float_as_uint(q1.z)) {  // an ancestor of p*
         float e, x;
-        box_interval(items[2 * q], q1, C, tmin, e, x);
+        box_interval(it_q0(items, q), q1, C, tmin, e, x);
         bad |= !(fminf(best, x) > e);
       }
     }
@@ -984,9 +989,9 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
       FastMat m;
       if (decided && bp >= 0) {
-        s0 = items9[2 * bp], s1 = items9[2 * bp + 1];
+        s0 = it_q0(items9, bp), s1 = it_q1(items9, V.n_items9_alloc, bp);
         m = V.mats[__float_as_int(s1.z)];
-        decided = bf_verify(items9, C, tmin, tmax, bp);
+        decided = bf_verify(items9, V.n_items9_alloc, C, tmin, tmax, bp);
       }
       if (!decided) {  // the exact scan
         int hit;

@@ -914,7 +914,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   HIP_OK(hipMalloc(&arena, total));
   d->b1_arena = arena;
   char *b = (char *)arena;
-  HIP_OK(hipMemcpy(b + off[0], H.items9.data(), sizes[0], hipMemcpyHostToDevice));
+  {  // on the device as two arrays: every item's q0, then every item's q1 (rt_book1.h: it_q0 / it_q1)
+    const size_t na = H.items9.size() / 2;
+    std::vector<float4> soa(2 * na);
+    for (size_t k = 0; k < na; k++) soa[k] = H.items9[2 * k], soa[na + k] = H.items9[2 * k + 1];
+    HIP_OK(hipMemcpy(b + off[0], soa.data(), sizes[0], hipMemcpyHostToDevice));
+  }
   if (sizes[1]) HIP_OK(hipMemcpy(b + off[1], H.mats.data(), sizes[1], hipMemcpyHostToDevice));
   b1::Book1View &V = d->b1view;
   memset(&V, 0, sizeof V);
