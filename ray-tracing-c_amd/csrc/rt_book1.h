@@ -338,14 +338,17 @@ constexpr uint32_t kLeaf9 = 0x80000000u;
 RT_D float4 it_q0(const float4 *items, uint32_t p) { return items[p]; }
 RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint32_t)na + p]; }
 
-RT_D bool trav_step_v9(const Book1View &V, const float4 *items, Lane &L, float tmin) {
+// items_q1 = items + V.n_items9_alloc, n = V.n_items9 (hoisted by the caller)
+RT_D bool trav_step_v9(const float4 *items, const float4 *items_q1, uint32_t n, Lane &L, float tmin) {
   const uint32_t p = L.cur;
-  float4 q0 = it_q0(items, p), q1 = it_q1(items, V.n_items9_alloc, p);
+  float4 q0 = items[p], q1 = items_q1[p];
   // both halves in one LDS round trip: without this the compiler sinks the q1.xy / q1.z reads into
   // the branches that use them, i.e. three dependent round trips per step.  (Reading the successor
   // one step ahead measured slower: its moves and the re-read after a skip cost more than the latency.)
   asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z), "+v"(q1.w));
   const uint32_t w = __float_as_uint(q1.w);
+  // (branches, not both tests straight-line for every lane: a wave's lanes are mostly at one kind --
+  // the straight-line step measured 1.3x slower)
   uint32_t next = p + 1;
   if (w & kLeaf9) {
     sphere_test_data(q0, (int)(w & 0x7fffffffu), L, tmin);
@@ -353,7 +356,7 @@ RT_D bool trav_step_v9(const Book1View &V, const float4 *items, Lane &L, float t
     if (!aabb_packed(q0, q1, L, tmin)) next = p + __float_as_uint(q1.z);
   }
   L.cur = next;
-  return next >= (uint32_t)V.n_items9;
+  return next >= n;
 }
 
 // ---------------------------------------------------------------- path record
@@ -1205,7 +1208,9 @@ constexpr int kSteps = 16;
 
 // The lane kernel.  kMode: 0 frame (whole pixels), 1 cost pre-pass (also counts draws per item),
 // 2 chain render (items of ch_items, or the continuation items of ch_cont).
-template <bool kLds, int kMode = 0>
+// kRecut: the run-time re-cut paths (RT_RECUT=1) compiled in -- a separate instantiation, so that
+// their registers do not enter the default chain kernel's loop (they cost it 8 SGPR reloads a step).
+template <bool kLds, int kMode = 0, bool kRecut = false>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
   const bool cont = kMode == 2 && V.ch_cont != nullptr;
@@ -1250,7 +1255,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   // intra-wave cuts (chain launches): handoff slots and idle masks in LDS behind the scene items
   uint2 *handoff = nullptr;
   unsigned long long *idle_lds = nullptr;
-  const bool cuts = kMode == 2 && V.recut_lanes != 0 && !cont;
+  const bool cuts = kRecut && kMode == 2 && V.recut_lanes != 0 && !cont;
   if (kMode == 2) {
     char *hb = lds + (kLds ? (size_t)V.n_items9_alloc * 2 * sizeof(float4) : 0);
     handoff = (uint2 *)hb;
@@ -1320,11 +1325,14 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     if (do_trav) {
       // ---------------- traversal steps for every lane still traversing
       if (mode == kTrav) {
+        const float4 *items_q1 = items9 + V.n_items9_alloc;
+        uint32_t n9 = (uint32_t)V.n_items9;
+        asm volatile("" : "+v"(n9));  // (in a VGPR: as an SGPR it was re-read from its spill lanes every step)
 #pragma unroll
         for (int u = 0; u < kSteps; u++)
           if (mode == kTrav) {
             if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
-            if (trav_step_v9(V, items9, L, tmin)) mode = kWait;
+            if (trav_step_v9(items9, items_q1, n9, L, tmin)) mode = kWait;
           }
       }
       continue;
@@ -1419,7 +1427,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         // no item left: a whole-wave helper's queued cut, if any (RecutReq); else this lane is done --
         // idle, where a lane of its wave may still hand it a cut of its own chain
         uint32_t cut = 0u, cut_pix = 0u;
-        if (kMode == 2 && item >= total_own && V.rq && !cuts) {
+        if (kRecut && kMode == 2 && item >= total_own && V.rq && !cuts) {
           const int req = recut_pop(V);
           if (req >= 0) {
             const RecutReq r = V.rq[(uint32_t)req];

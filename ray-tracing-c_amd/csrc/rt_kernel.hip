@@ -91,10 +91,10 @@ __global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
-template <bool kLds>
+template <bool kLds, bool kRecut = false>
 __global__ __launch_bounds__(b1::kBlock, 4) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  b1::render_batched<kLds, 2>(V, out, lds);
+  b1::render_batched<kLds, 2, kRecut>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
 template <bool kLds>
@@ -1188,6 +1188,11 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
 static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
   const size_t lds = d->b1_lds_bytes, bytes = lds + b1::kHandoffBytes;  // (+ the intra-wave cut handoff)
+  if (V.recut_lanes || V.rq) {  // RT_RECUT=1: the instantiation with the re-cut paths
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, true>), gc, blk, bytes, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, true>), gc, blk, bytes, st, V, d_out);
+    return;
+  }
   if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, bytes, st, V, d_out);
   else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, bytes, st, V, d_out);
 }
