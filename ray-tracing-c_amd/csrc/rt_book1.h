@@ -158,6 +158,7 @@ struct Book1View {
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
+  int32_t cost_time;         // cost pre-pass: cost = the pixel's wall-clock latency (10-ns ticks), not its steps
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
@@ -338,10 +339,10 @@ constexpr uint32_t kLeaf9 = 0x80000000u;
 RT_D float4 it_q0(const float4 *items, uint32_t p) { return items[p]; }
 RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint32_t)na + p]; }
 
-// items_q1 = items + V.n_items9_alloc, n = V.n_items9 (hoisted by the caller)
-RT_D bool trav_step_v9(const float4 *items, const float4 *items_q1, uint32_t n, Lane &L, float tmin) {
+// na = V.n_items9_alloc, n = V.n_items9 (hoisted by the caller, in VGPRs)
+RT_D bool trav_step_v9(const float4 *items, uint32_t na, uint32_t n, Lane &L, float tmin) {
   const uint32_t p = L.cur;
-  float4 q0 = items[p], q1 = items_q1[p];
+  float4 q0 = items[p], q1 = items[na + p];
   // both halves in one LDS round trip: without this the compiler sinks the q1.xy / q1.z reads into
   // the branches that use them, i.e. three dependent round trips per step.  (Reading the successor
   // one step ahead measured slower: its moves and the re-read after a skip cost more than the latency.)
@@ -1265,6 +1266,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const int wave_in_block = tid >> 6;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
+  uint32_t px_t0 = 0;  // (cost pre-pass, cost_time: the pixel's start)
   int32_t pix = 0;  // (< 2^31: host-checked)
   int s = 0, depth = 0;
   Pcg32 g;
@@ -1323,17 +1325,35 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     }
 #endif
     if (do_trav) {
-      // ---------------- traversal steps for every lane still traversing
-      if (mode == kTrav) {
-        const float4 *items_q1 = items9 + V.n_items9_alloc;
-        uint32_t n9 = (uint32_t)V.n_items9;
-        asm volatile("" : "+v"(n9));  // (in a VGPR: as an SGPR it was re-read from its spill lanes every step)
+      // ---------------- traversal steps for every lane still traversing: pass after pass in this
+      // inner loop while the wave's shading batch is not full (back through the outer loop's merge
+      // after every pass, the compiler shuffled ~90 registers per pass: 6 % of the frame)
+      // (in VGPRs: as SGPRs they were re-read from their spill lanes every step)
+      uint32_t n9 = (uint32_t)V.n_items9, na = (uint32_t)V.n_items9_alloc;
+      asm volatile("" : "+v"(n9), "+v"(na));
+      for (;;) {
+        if (mode == kTrav) {
 #pragma unroll
-        for (int u = 0; u < kSteps; u++)
-          if (mode == kTrav) {
-            if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
-            if (trav_step_v9(items9, items_q1, n9, L, tmin)) mode = kWait;
-          }
+          for (int u = 0; u < kSteps; u++)
+            if (mode == kTrav) {
+              if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
+              if (trav_step_v9(items9, na, n9, L, tmin)) mode = kWait;
+            }
+        }
+        if (cuts) break;  // (the loop top hands cuts to idle lanes between passes)
+        const uint64_t t2 = __ballot(mode == kTrav), w2 = __ballot(mode == kWait);
+        const int batch2 = min(V.shade_batch, (3 * (int)__popcll(t2 | w2) + 3) / 4);
+        if (t2 == 0ull || (int)__popcll(w2) >= batch2) break;
+#ifdef RT_LOOP_STATS
+        {
+          const uint64_t now = clock64();
+          st_cyc[0] += now - st_last;
+          st_last = now;
+          st_it[0]++;
+          st_lanes[0] += (uint32_t)__popcll(t2);
+          st_live += (uint32_t)__popcll(t2 | w2);
+        }
+#endif
       }
       continue;
     }
@@ -1390,8 +1410,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          if (kMode == 1)
-            V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
+          if (kMode == 1) {
+            const uint32_t c = V.cost_time ? (uint32_t)wall_clock64() - px_t0 : px_steps;
+            V.cost_out[pix] = cut ? (uint32_t)((uint64_t)c * spp / s) : c;
+          }
           if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
@@ -1471,6 +1493,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         need_pixel = false;
         px_steps = 0;
+        if (kMode == 1) px_t0 = (uint32_t)wall_clock64();
         if (V.px_time && kMode != 2) V.px_time[2 * pix] = (uint32_t)wall_clock64();
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }

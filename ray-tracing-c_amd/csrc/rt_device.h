@@ -57,18 +57,21 @@ RT_D f3 ray_at(f3 o, f3 d, float t) { return add(o, scale(d, t)); }
 
 // ------------------------------------------------------------------------------ pcg32
 struct Pcg32 {
-  uint64_t state, inc;
+  // inc = (initseq << 1) | 1 kept in 32 bits: every seed's initseq is 23 + a pixel column (< 2^30,
+  // host-checked image sizes), so the upper half is zero -- one register less per lane
+  uint64_t state;
+  uint32_t inc;
   uint32_t n;  // draws since seed(): the stream offset (split render, rt_book1.h); dead code elsewhere
   RT_D uint32_t next() {
     const uint64_t s = state;
-    state = s * 6364136223846793005ULL + inc;
+    state = s * 6364136223846793005ULL + (uint64_t)inc;
     n++;
     const uint32_t x = (uint32_t)(((s >> 18u) ^ s) >> 27u);
     return __builtin_rotateright32(x, (uint32_t)(s >> 59u));
   }
   RT_D void seed(uint64_t initstate, uint64_t initseq) {
     state = 0u;
-    inc = (initseq << 1u) | 1u;
+    inc = (uint32_t)((initseq << 1u) | 1u);
     (void)next();
     state += initstate;
     (void)next();
@@ -77,7 +80,7 @@ struct Pcg32 {
   // advance by k draws without generating them: the LCG's k-step map (a^k, c*(a^k-1)/(a-1)) by
   // squaring, O(log k) 64-bit multiplies (pcg32_advance semantics)
   RT_D void skip(uint32_t k) {
-    uint64_t am = 6364136223846793005ULL, ac = inc, mul = 1u, add = 0u;
+    uint64_t am = 6364136223846793005ULL, ac = (uint64_t)inc, mul = 1u, add = 0u;
     for (uint32_t r = k; r != 0u; r >>= 1) {
       if (r & 1u) mul *= am, add = add * am + ac;
       ac = (am + 1u) * ac;

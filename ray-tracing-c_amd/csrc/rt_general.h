@@ -25,7 +25,7 @@ struct GeneralView {
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
   int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
   int32_t flat;              // kBatch: common entries as one straight-line block (pre_common) plus up to
-                             // flat - 1 box entries in the same step (RT_GEN_FLAT; 0: branched dispatch)
+                             // flat - 1 box entries in the same step (RT_GEN_FLAT, >= 1)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
   int32_t perlin_lds;        // kAllLds: byte offset of perlins[0]'s LDS copy (PerlinLds) behind the preorder; -1: none
   float4 *xrec;              // explicit albedos of path records: kMaxDepth per thread of the grid, thread-contiguous
@@ -550,18 +550,14 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           if ((rm | cm) == 0) break;
           const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
           bool fin = false;
-          if (V.flat) {
-            GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
-            gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
-            GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
-            gs_c = GS_NOW();
-            if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
-            GS_ADD(kGsCycRare, GS_NOW() - gs_c);
-            GS_ADD(kGsRareSteps, run_rare);
-          } else if (tracing && (!rare || run_rare)) {
-            fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
-          }
+          GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
+          gs_c = GS_NOW();
+          if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
+          GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
+          gs_c = GS_NOW();
+          if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+          GS_ADD(kGsCycRare, GS_NOW() - gs_c);
+          GS_ADD(kGsRareSteps, run_rare);
           if (fin) {
             tracing = false;
             pending = true;

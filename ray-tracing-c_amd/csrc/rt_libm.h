@@ -42,6 +42,20 @@ RT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 RT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
 RT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
 RT_HD double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+// A double constant materialized at its use, by two v_mov_b32 of its halves inside a volatile asm
+// (which the compiler cannot hoist): otherwise it hoists the constant addends of the polynomials
+// below out of the render loops into VGPR pairs that live across the whole kernel and spill, since
+// v_fmac_f64 overwrites its addend register.  KD(lo, hi): the constant's 32-bit halves.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KD(LO, HI)                                                                          \
+  ({                                                                                        \
+    uint32_t kd_lo_, kd_hi_;                                                                \
+    asm volatile("v_mov_b32 %0, " #LO "\n\tv_mov_b32 %1, " #HI : "=v"(kd_lo_), "=v"(kd_hi_)); \
+    __builtin_bit_cast(double, ((uint64_t)kd_hi_ << 32) | kd_lo_);                          \
+  })
+#else
+#define KD(LO, HI) __builtin_bit_cast(double, ((uint64_t)(HI) << 32) | (uint64_t)(LO))
+#endif
 
 // ---------------------------------------------------------------- sincosf / sinf
 // sincos_t layout: sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4  (14 doubles, 2 copies).
@@ -75,19 +89,24 @@ RT_HD uint32_t inv_pio4(int i) {
 RT_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ff; }
 
 // sincosf_poly with the FMA contraction of __sincosf_fma: returns (sin, cos) of the reduced
-// argument, already swapped for odd quadrants.
-RT_HD void sincos_poly(double x, double x2, const SinCosTab &p, int n, float *sinp, float *cosp) {
+// argument, already swapped for odd quadrants.  neg_c: table 1 (quadrants with n & 2), whose cos
+// coefficients are table 0's negated -- every fma of the cos half then yields exactly the negated
+// value (round-to-nearest is symmetric; no intermediate is zero: the reduced |x| <= pi/4), so the
+// polynomial runs on table 0's constants, materialized at their use (KD), and cv is negated.
+RT_HD void sincos_poly(double x, double x2, bool neg_c, int n, float *sinp, float *cosp) {
+  const SinCosTab &p = sincos_tab(0);
   double x3 = x2 * x;
   double x4 = x2 * x2;
-  double s1 = fmad(x2, p.s3, p.s2);
-  double c2 = fmad(x2, p.c4, p.c3);
-  double c1 = fmad(x2, p.c1, p.c0);
+  double s1 = fmad(x2, p.s3, KD(0x05230bc4, 0x3f811076) /* s2 = 0x1.1107605230bc4p-7 */);
+  double c2 = fmad(x2, p.c4, KD(0xe89a359d, 0xbf56c087) /* c3 = -0x1.6c087e89a359dp-10 */);
+  double c1 = fmad(x2, p.c1, KD(0x0, 0x3ff00000) /* c0 = 1 */);
   double x5 = x3 * x2;
   double x6 = x4 * x2;
   double s = fmad(x3, p.s1, x);
   double c = fmad(x4, p.c2, c1);
   float sv = (float)fmad(s1, x5, s);
-  float cv = (float)fmad(c2, x6, c);
+  double cd = fmad(c2, x6, c);
+  float cv = (float)(neg_c ? -cd : cd);
   if (n & 1) { *sinp = cv; *cosp = sv; }
   else { *sinp = sv; *cosp = cv; }
 }
@@ -130,19 +149,17 @@ RT_HD void sincosf(float y, float *sinp, float *cosp) {
       *cosp = 1.0f;
       return;
     }
-    sincos_poly(x, x2, sincos_tab(0), 0, sinp, cosp);
+    sincos_poly(x, x2, false, 0, sinp, cosp);
   } else if (at < 0x42f) {                // |y| < 120
     x = reduce_fast(x, sincos_tab(0), &n);
     const double s = sincos_tab(0).sign[n & 3];
-    const SinCosTab &p = sincos_tab((n & 2) ? 1 : 0);
-    sincos_poly(x * s, x * x, p, n, sinp, cosp);
+    sincos_poly(x * s, x * x, (n & 2) != 0, n, sinp, cosp);
   } else if (at < 0x7f8) {                // finite
     const uint32_t xi = f2u(y);
     const int sign = xi >> 31;
     x = reduce_large(xi, &n);
     const double s = sincos_tab(0).sign[(n + sign) & 3];
-    const SinCosTab &p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    sincos_poly(x * s, x * x, p, n, sinp, cosp);
+    sincos_poly(x * s, x * x, ((n + sign) & 2) != 0, n, sinp, cosp);
   } else {
     *sinp = *cosp = y - y;
   }
@@ -208,8 +225,8 @@ RT_HD double powf_log2_inline(uint32_t ix) {
   const double r = fmad(z, invc, -1.0);
   const double y0 = (double)k + logc;
   const double r2 = r * r;
-  double y = fmad(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
-  const double p = fmad(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+  double y = fmad(0x1.27616c9496e0bp-2, r, KD(0xa075c67a, 0xbfd71969) /* -0x1.71969a075c67ap-2 */);
+  const double p = fmad(0x1.ec70a6ca7baddp-2, r, KD(0x48bef6c8, 0xbfe71547) /* -0x1.7154748bef6c8p-1 */);
   const double r4 = r2 * r2;
   double q = fmad(0x1.71547652ab82bp+0, r, y0);
   q = fmad(p, r2, q);
@@ -227,9 +244,9 @@ RT_HD double powf_exp2_inline(double xd, uint32_t sign_bias) {
   const uint64_t ski = ki + sign_bias;
   t += ski << (52 - 5);
   const double s = u2d(t);
-  const double z = fmad(0x1.c6af84b912394p-5, r, 0x1.ebfce50fac4f3p-3);
+  const double z = fmad(0x1.c6af84b912394p-5, r, KD(0x50fac4f3, 0x3fcebfce) /* 0x1.ebfce50fac4f3p-3 */);
   const double r2 = r * r;
-  double y = fmad(0x1.62e42ff0c52d6p-1, r, 1.0);
+  double y = fmad(0x1.62e42ff0c52d6p-1, r, KD(0x0, 0x3ff00000) /* 1.0 */);
   y = fmad(z, r2, y);
   return y * s;
 }
@@ -306,7 +323,7 @@ RT_HD float logf(float x) {
   const double r = fmad(z, invc, -1.0);
   const double y0 = fmad((double)k, 0x1.62e42fefa39efp-1, logc);
   const double r2 = r * r;
-  double y = fmad(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
+  double y = fmad(0x1.5575b0be00b6ap-2, r, KD(0xf20a4123, 0xbfdffffe) /* -0x1.ffffef20a4123p-2 */);
   y = fmad(-0x1.00ea348b88334p-2, r2, y);
   y = fmad(y, r2, y0 + r);
   return (float)y;

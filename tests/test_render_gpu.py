@@ -264,7 +264,7 @@ def test_chain_render_north_star_scene(manifest, env, monkeypatch):
 
 @pytest.mark.parametrize("env", [{"RT_GEN_PRE": "0"}, {"RT_GEN_BATCH": "0"}, {"RT_GEN_BATCH": "1", "RT_GEN_STEPS": "1"},
                                  {"RT_GEN_BATCH": "64", "RT_GEN_STEPS": "32"}, {"RT_LPT": "0"}, {"RT_GEN_LDS": "0"},
-                                 {"RT_GEN_LDS": "7"}, {"RT_GEN_LDS": "2048"}, {"RT_GEN_FLAT": "0"},
+                                 {"RT_GEN_LDS": "7"}, {"RT_GEN_LDS": "2048"}, {"RT_GEN_FLAT": "2"},
                                  {"RT_GEN_FLAT": "1"}, {"RT_GEN_FLAT": "6"}, {"RT_GEN_RARE": "1"}, {"RT_GEN_RARE": "64", "RT_GEN_STEPS": "3"}])
 @pytest.mark.parametrize("name", ["s5_200x112_16spp_d50", "s6_200x200_16spp_d50", "s7_200x200_8spp_d50"])
 def test_general_path_variants(manifest, name, env, monkeypatch):
