@@ -532,36 +532,46 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           break;  // the first step of the iteration only
         }
 #endif
+        // iteration after iteration in this inner loop while the shading batch is not full (back
+        // through the outer loop's merge after every iteration, the compiler shuffled the lanes'
+        // trace state between register sets every step)
+        for (;;) {
 #pragma unroll 1
-        for (int k = 0; k < V.steps; k++) {
-          gs_c = GS_NOW();
-          float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q1 = q0;
-          bool rare = false;
-          if (tracing) {
-            const uint32_t q = T.p < (uint32_t)S.n_pre ? T.p : 0u;
-            if (kAllLds || q < n_lds) {
-              q0 = lds[2 * q], q1 = lds[2 * q + 1];
-            } else {
-              q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
+          for (int k = 0; k < V.steps; k++) {
+            gs_c = GS_NOW();
+            float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q1 = q0;
+            bool rare = false;
+            if (tracing) {
+              const uint32_t q = T.p < (uint32_t)S.n_pre ? T.p : 0u;
+              if (kAllLds || q < n_lds) {
+                q0 = lds[2 * q], q1 = lds[2 * q + 1];
+              } else {
+                q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
+              }
+              rare = pre_is_rare<F>(T, q1);
             }
-            rare = pre_is_rare<F>(T, q1);
+            const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
+            if ((rm | cm) == 0) break;
+            const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
+            bool fin = false;
+            GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
+            gs_c = GS_NOW();
+            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
+            GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
+            gs_c = GS_NOW();
+            if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+            GS_ADD(kGsCycRare, GS_NOW() - gs_c);
+            GS_ADD(kGsRareSteps, run_rare);
+            if (fin) {
+              tracing = false;
+              pending = true;
+            }
           }
-          const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
-          if ((rm | cm) == 0) break;
-          const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);
-          bool fin = false;
-          GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
-          gs_c = GS_NOW();
-          if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
-          GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
-          gs_c = GS_NOW();
-          if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
-          GS_ADD(kGsCycRare, GS_NOW() - gs_c);
-          GS_ADD(kGsRareSteps, run_rare);
-          if (fin) {
-            tracing = false;
-            pending = true;
-          }
+          const uint64_t tr2 = __ballot(!done && tracing), ready2 = __ballot(!done && !tracing);
+          const int batch2 = min(V.batch, (3 * (int)__popcll(tr2 | ready2) + 3) / 4);
+          if (tr2 == 0ull || (int)__popcll(ready2) >= batch2) break;
+          GS_ADD(kGsTraceIters, 1);
+          GS_ADD(kGsTraceLanes, __popcll(tr2));
         }
         continue;
       }
