@@ -158,7 +158,6 @@ struct Book1View {
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
-  int32_t cost_time;         // cost pre-pass: cost = the pixel's wall-clock latency (10-ns ticks), not its steps
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
@@ -1266,7 +1265,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const int wave_in_block = tid >> 6;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
-  uint32_t px_t0 = 0;  // (cost pre-pass, cost_time: the pixel's start)
   int32_t pix = 0;  // (< 2^31: host-checked)
   int s = 0, depth = 0;
   Pcg32 g;
@@ -1410,10 +1408,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          if (kMode == 1) {
-            const uint32_t c = V.cost_time ? (uint32_t)wall_clock64() - px_t0 : px_steps;
-            V.cost_out[pix] = cut ? (uint32_t)((uint64_t)c * spp / s) : c;
-          }
+          if (kMode == 1)
+            V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
           if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
@@ -1493,7 +1489,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         need_pixel = false;
         px_steps = 0;
-        if (kMode == 1) px_t0 = (uint32_t)wall_clock64();
         if (V.px_time && kMode != 2) V.px_time[2 * pix] = (uint32_t)wall_clock64();
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }

@@ -539,17 +539,18 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
 #pragma unroll 1
           for (int k = 0; k < V.steps; k++) {
             gs_c = GS_NOW();
-            float4 q0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q1 = q0;
-            bool rare = false;
-            if (tracing) {
-              const uint32_t q = T.p < (uint32_t)S.n_pre ? T.p : 0u;
-              if (kAllLds || q < n_lds) {
-                q0 = lds[2 * q], q1 = lds[2 * q + 1];
-              } else {
-                q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
-              }
-              rare = pre_is_rare<F>(T, q1);
+            // every lane loads (entry 0 when not tracing): both halves as two b128 reads in one round
+            // trip (left to itself the compiler split them into four narrower reads)
+            const uint32_t q = tracing && T.p < (uint32_t)S.n_pre ? T.p : 0u;
+            float4 q0, q1;
+            if (kAllLds || q < n_lds) {
+              q0 = lds[2 * q], q1 = lds[2 * q + 1];
+            } else {
+              q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
             }
+            asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z),
+                         "+v"(q1.w));
+            const bool rare = tracing && pre_is_rare<F>(T, q1);
             const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
             if ((rm | cm) == 0) break;
             const bool run_rare = rm != 0 && (cm == 0 || (int)__popcll(rm) >= V.rare_min || k == V.steps - 1);

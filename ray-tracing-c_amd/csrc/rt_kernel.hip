@@ -552,12 +552,10 @@ struct Config {
   int recut_min = 32;      //   of chains with at least this many samples left
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
-  bool cost_time = false;  // cost pre-pass: a pixel's cost is its measured latency, not its steps
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
-    c.cost_time = env_flag("RT_COST_TIME", c.cost_time);
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -1181,7 +1179,6 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.cost_out = d->lpt_cost;
   P.draw_out = d->draw_out;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
-  P.cost_time = d->cfg.cost_time ? 1 : 0;
   P.n_coop = nullptr;
   // at the chain kernel's occupancy, on its grid
   const dim3 g((unsigned)d->chain_grid), blk(b1::kBlock);
@@ -1239,11 +1236,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.lat = kLaneLat;
   m.thr = kLaneThr;
   m.coop = kCoopStep;
-  if (cfg.cost_time) {  // costs are latencies under load: the throughput time is their sum over the lanes
-    m.lat = 1.0f;
-    m.thr = 1.0f;
-    m.coop = kCoopStep / kLaneLat;
-  }
   m.beta = cfg.chain_beta;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
