@@ -294,9 +294,9 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
   return next >= n;
 }
 
-// The common entries (BVH box, sphere, quad) as one straight-line block: every lane evaluates the
-// box slabs, the sphere roots and the quad plane for its entry and keeps the result of its kind, so
-// a wave whose lanes sit at all three kinds (nearly every step at scene 7) runs no kind branches;
+// The common entries (BVH box, sphere, quad) as one block: every lane evaluates the box slabs, and
+// the sphere roots and the quad plane when any lane of the wave sits at a sphere / quad (wave-
+// uniform branches), for its entry and keeps the result of its kind -- no per-lane kind branches;
 // only the quad's in-plane test (its record: measured no faster when loaded up front) and the
 // sphere's out-of-range fallback branch.
 // Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
@@ -314,24 +314,29 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   const float lo = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? bx : ax), iy < 0 ? by : ay), iz < 0 ? bz : az);
   const float hi = fminf(fminf(fminf(T.tmax, ix < 0 ? ax : bx), iy < 0 ? ay : by), iz < 0 ? az : bz);
   const bool skip = ((F & RT_FEAT_BVH) && kind == RT_KIND_BVH) && hi <= lo;
-  // sphere: q0 = (center, r^2)
-  const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
-  const float b = dot(oc, d);
-  const float c = dot(oc, oc) - q0.w;
-  const float disc = b * b - T.dd * c;
-  float sq = sqrt_core(disc);
-  float r1 = div_core(-b - sq, T.dd, T.ra), r2 = div_core(-b + sq, T.dd, T.ra);
-  const bool ok = (int)T.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
-                  (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
-  if (__builtin_expect(kind == RT_KIND_SPHERE && !(disc < 0) && !ok, 0)) {
-    sq = sqrtf(disc);
-    r1 = (-b - sq) / T.dd;
-    r2 = (-b + sq) / T.dd;
+  // sphere: q0 = (center, r^2); quad: q0 = (normal, D), the record only past the plane test.  Each
+  // block runs only when a lane of the wave sits at its kind (a wave-uniform branch: scene 7 +3 %)
+  bool hit = false;
+  float t = 0.0f;
+  if (__ballot(kind == RT_KIND_SPHERE) != 0ull) {
+    const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
+    const float b = dot(oc, d);
+    const float c = dot(oc, oc) - q0.w;
+    const float disc = b * b - T.dd * c;
+    float sq = sqrt_core(disc);
+    float r1 = div_core(-b - sq, T.dd, T.ra), r2 = div_core(-b + sq, T.dd, T.ra);
+    const bool ok = (int)T.fast & ((int)(disc == 0.0f) | ((int)(disc >= kSqrtLo) & (int)(disc <= __FLT_MAX__))) &
+                    (int)(fabsf(-b - sq) <= kNumHi) & (int)(fabsf(-b + sq) <= kNumHi);
+    if (__builtin_expect(kind == RT_KIND_SPHERE && !(disc < 0) && !ok, 0)) {
+      sq = sqrtf(disc);
+      r1 = (-b - sq) / T.dd;
+      r2 = (-b + sq) / T.dd;
+    }
+    const bool take1 = !(r1 <= tmin || r1 >= T.tmax), take2 = !(r2 <= tmin || r2 >= T.tmax);
+    hit = kind == RT_KIND_SPHERE && !(disc < 0) && (take1 || take2);
+    t = take1 ? r1 : r2;
   }
-  const bool take1 = !(r1 <= tmin || r1 >= T.tmax), take2 = !(r2 <= tmin || r2 >= T.tmax);
-  bool hit = kind == RT_KIND_SPHERE && !(disc < 0) && (take1 || take2);
-  float t = take1 ? r1 : r2;
-  if (F & RT_FEAT_QUAD) {  // quad: q0 = (normal, D); the record only past the plane test
+  if ((F & RT_FEAT_QUAD) && __ballot(kind == RT_KIND_QUAD) != 0ull) {
     const f3 nq = mk(q0.x, q0.y, q0.z);
     const float denom = dot(nq, d);
     const float tt = (q0.w - dot(nq, o)) / denom;
