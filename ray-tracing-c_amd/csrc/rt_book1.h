@@ -248,7 +248,7 @@ struct Lane {         // plain scalars: an f3 member here was kept in scratch by
   float ra;           // refined reciprocal of a (div_core), hoisted per ray
   bool fast;          // a in the range where div_core == '/'
   int32_t hit;        // sphere index or -1
-  uint32_t cur;       // preorder item being visited
+  uint32_t cur;       // preorder item being visited (byte offset: index x 16)
 };
 
 // AABB_hit with the slabs evaluated together: t_min / t_max only tighten and fmaxf/fminf ignore a
@@ -338,25 +338,30 @@ constexpr uint32_t kLeaf9 = 0x80000000u;
 RT_D float4 it_q0(const float4 *items, uint32_t p) { return items[p]; }
 RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint32_t)na + p]; }
 
-// na = V.n_items9_alloc, n = V.n_items9 (hoisted by the caller, in VGPRs)
-RT_D bool trav_step_v9(const float4 *items, uint32_t na, uint32_t n, Lane &L, float tmin) {
+// L.cur, na16 and n16 are byte offsets (item index x 16): na16 = 16 V.n_items9_alloc, n16 = 16 V.n_items9
+// (hoisted by the caller, in VGPRs) -- the step then needs no index scaling
+RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L, float tmin) {
   const uint32_t p = L.cur;
-  float4 q0 = items[p], q1 = items[na + p];
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const char *base = (const char *)items;
+  f4v v0 = *(const f4v *)(base + p), v1 = *(const f4v *)(base + na16 + p);
   // both halves in one LDS round trip: without this the compiler sinks the q1.xy / q1.z reads into
   // the branches that use them, i.e. three dependent round trips per step.  (Reading the successor
   // one step ahead measured slower: its moves and the re-read after a skip cost more than the latency.)
-  asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z), "+v"(q1.w));
+  // (whole 128-bit tuples: per-component constraints made the compiler shuffle registers after the loads)
+  asm volatile("" : "+v"(v0), "+v"(v1));
+  const float4 q0 = make_float4(v0.x, v0.y, v0.z, v0.w), q1 = make_float4(v1.x, v1.y, v1.z, v1.w);
   const uint32_t w = __float_as_uint(q1.w);
   // (branches, not both tests straight-line for every lane: a wave's lanes are mostly at one kind --
   // the straight-line step measured 1.3x slower)
-  uint32_t next = p + 1;
+  uint32_t next = p + 16u;
   if (w & kLeaf9) {
     sphere_test_data(q0, (int)(w & 0x7fffffffu), L, tmin);
   } else {
-    if (!aabb_packed(q0, q1, L, tmin)) next = p + __float_as_uint(q1.z);
+    if (!aabb_packed(q0, q1, L, tmin)) next = p + (__float_as_uint(q1.z) << 4);
   }
   L.cur = next;
-  return next >= n;
+  return next >= n16;
 }
 
 // ---------------------------------------------------------------- path record
@@ -1256,7 +1261,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   uint2 *handoff = nullptr;
   unsigned long long *idle_lds = nullptr;
   const bool cuts = kRecut && kMode == 2 && V.recut_lanes != 0 && !cont;
-  if (kMode == 2) {
+  if (kMode == 2 && kRecut) {  // (the default instantiation has no handoff region: occupancy 5 needs the LDS)
     char *hb = lds + (kLds ? (size_t)V.n_items9_alloc * 2 * sizeof(float4) : 0);
     handoff = (uint2 *)hb;
     idle_lds = (unsigned long long *)(hb + kBlock * sizeof(uint2));
@@ -1327,7 +1332,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       // inner loop while the wave's shading batch is not full (back through the outer loop's merge
       // after every pass, the compiler shuffled ~90 registers per pass: 6 % of the frame)
       // (in VGPRs: as SGPRs they were re-read from their spill lanes every step)
-      uint32_t n9 = (uint32_t)V.n_items9, na = (uint32_t)V.n_items9_alloc;
+      uint32_t n9 = (uint32_t)V.n_items9 * 16u, na = (uint32_t)V.n_items9_alloc * 16u;  // (bytes)
       asm volatile("" : "+v"(n9), "+v"(na));
       for (;;) {
         if (mode == kTrav) {

@@ -547,14 +547,17 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             // every lane loads (entry 0 when not tracing): both halves as two b128 reads in one round
             // trip (left to itself the compiler split them into four narrower reads)
             const uint32_t q = tracing && T.p < (uint32_t)S.n_pre ? T.p : 0u;
-            float4 q0, q1;
+            // (the barrier on whole 128-bit tuples: per-component constraints made the compiler shuffle
+            // registers after the loads)
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            f4v v0, v1;
             if (kAllLds || q < n_lds) {
-              q0 = lds[2 * q], q1 = lds[2 * q + 1];
+              v0 = *(const f4v *)&lds[2 * q], v1 = *(const f4v *)&lds[2 * q + 1];
             } else {
-              q0 = S.pre[2 * q], q1 = S.pre[2 * q + 1];
+              v0 = *(const f4v *)&S.pre[2 * q], v1 = *(const f4v *)&S.pre[2 * q + 1];
             }
-            asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z),
-                         "+v"(q1.w));
+            asm volatile("" : "+v"(v0), "+v"(v1));
+            float4 q0 = make_float4(v0.x, v0.y, v0.z, v0.w), q1 = make_float4(v1.x, v1.y, v1.z, v1.w);
             const bool rare = tracing && pre_is_rare<F>(T, q1);
             const uint64_t rm = __ballot(tracing && rare), cm = __ballot(tracing && !rare);
             if ((rm | cm) == 0) break;

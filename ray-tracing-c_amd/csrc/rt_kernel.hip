@@ -84,21 +84,23 @@ __global__ __launch_bounds__(kBlock) void rt_render_deep_kernel(DScene S, int ro
 }
 
 // Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.  The
-// chain kernel and its cost pre-pass run at 4 waves per SIMD (128 VGPRs: no spills in the loop; 5 waves
-// spilled and measured slower); the lane kernel at 5.
+// chain kernel, its cost pre-pass and the lane kernel run at 5 waves per SIMD (96 VGPRs; the chain
+// kernel spills 15, none in the traversal loop: 270 ms vs 282 ms at 4 waves; with the
+// SLP vectorizer's packed f32 ops it needed 128 and spilled 65 at 5); the re-cut variant at 4 (its
+// intra-wave handoff region in LDS does not fit 5 workgroups beside the scene).
 template <bool kLds>
 __global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
 template <bool kLds, bool kRecut = false>
-__global__ __launch_bounds__(b1::kBlock, 4) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+__global__ __launch_bounds__(b1::kBlock, kRecut ? 4 : 5) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 2, kRecut>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
 template <bool kLds>
-__global__ __launch_bounds__(b1::kBlock, 4) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 1>(V, out, lds);
 }
@@ -115,7 +117,8 @@ __global__ __launch_bounds__(256) void chain_fold_kernel(b1::Book1View V, uint8_
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
 // kThreads = kBigBlock: one 768-thread workgroup per CU (3 waves per SIMD, as the 256-thread variant
 // at occupancy 3) holding the scene's WHOLE preorder in LDS (up to 160 KiB per workgroup on gfx950;
-// scene 7's 4946 entries are 158 KiB), so no traversal step waits on L2.
+// scene 7's 4946 entries are 158 KiB), so no traversal step waits on L2.  (1024 threads, 4 waves per
+// SIMD at 128 VGPRs without spills: 3.91 s vs 3.61-3.66 s for config 5)
 constexpr int kBigBlock = 768;
 template <int F, bool kBatch = false, int kThreads = gen::kBlock>
 __global__ __launch_bounds__(kThreads, kThreads == gen::kBlock ? (kBatch ? 3 : 1) : 1) void rt_general_kernel(
@@ -890,9 +893,14 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock,
       d->b1_lds_bytes));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
-      b1::kBlock, d->b1_lds_bytes + b1::kHandoffBytes));
+  if (cfg.recut)  // (the re-cut instantiation: occupancy 4, the intra-wave cut handoff behind the scene)
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true, true> : (const void *)rt_book1_chain_kernel<false, true>,
+        b1::kBlock, d->b1_lds_bytes + b1::kHandoffBytes));
+  else
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
+        b1::kBlock, d->b1_lds_bytes));
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   const int spill_grid = d->b1_grid > d->chain_grid ? d->b1_grid : d->chain_grid;
@@ -1189,13 +1197,13 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
 static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
   const size_t lds = d->b1_lds_bytes, bytes = lds + b1::kHandoffBytes;  // (+ the intra-wave cut handoff)
-  if (V.recut_lanes || V.rq) {  // RT_RECUT=1: the instantiation with the re-cut paths
+  if (d->cfg.recut) {  // RT_RECUT=1: the instantiation with the re-cut paths
     if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, true>), gc, blk, bytes, st, V, d_out);
     else hipLaunchKernelGGL((rt_book1_chain_kernel<false, true>), gc, blk, bytes, st, V, d_out);
     return;
   }
-  if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, bytes, st, V, d_out);
-  else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, bytes, st, V, d_out);
+  if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, lds, st, V, d_out);
+  else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, V, d_out);
 }
 
 // Records of a chain launch: grown on demand, up to the RT_CHAIN_MB budget (the planner keeps
