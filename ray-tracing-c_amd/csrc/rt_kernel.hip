@@ -93,8 +93,8 @@ __global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
-template <bool kLds, bool kRecut = false>
-__global__ __launch_bounds__(b1::kBlock, kRecut ? 4 : 5) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, bool kRecut = false, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kRecut ? 4 : kOcc) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 2, kRecut>(V, out, lds);
 }
@@ -555,6 +555,8 @@ struct Config {
   int recut_min = 32;      //   of chains with at least this many samples left
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
+  int chain_occ = 0;          // chain kernel waves per SIMD: 4, 5, or 0 = by pixels per lane (below)
+  float chain_occ_px = 0.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
@@ -603,6 +605,8 @@ struct Config {
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
+    c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ);
+    c.chain_occ_px = env_float("RT_CHAIN_OCC_PX", c.chain_occ_px);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
     c.gen_batch = env_int("RT_GEN_BATCH", 56);
@@ -637,7 +641,8 @@ struct rt_device_scene {
   b1::Book1View b1view;
   void *b1_arena = nullptr;
   size_t b1_lds_bytes = 0;
-  int b1_grid = 0, chain_grid = 0;
+  int b1_grid = 0, chain_grid = 0;  // chain_grid: the current chain launch's (one of the two below)
+  int chain_grid5 = 0, chain_grid4 = 0, chain_occ = 5;  // chain kernel grids at 5 / 4 waves per SIMD
   uint32_t *lpt_cost = nullptr;  // pre-pass steps per work item (W*H)
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
@@ -889,7 +894,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->b1_lds_bytes = align_up(lds ? items_bytes : 0, 16);
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
-  int per_cu = 0, per_cu_chain = 0;
+  int per_cu = 0, per_cu_chain = 0, per_cu_chain4 = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock,
       d->b1_lds_bytes));
@@ -901,9 +906,16 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
         b1::kBlock, d->b1_lds_bytes));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu_chain4, lds ? (const void *)rt_book1_chain_kernel<true, false, 4> : (const void *)rt_book1_chain_kernel<false, false, 4>,
+      b1::kBlock, d->b1_lds_bytes));
+  if (cfg.recut) per_cu_chain4 = per_cu_chain;  // (one instantiation, occupancy 4)
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
-  d->chain_grid = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
-  const int spill_grid = d->b1_grid > d->chain_grid ? d->b1_grid : d->chain_grid;
+  d->chain_grid5 = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
+  d->chain_grid4 = prop.multiProcessorCount * (per_cu_chain4 < 1 ? 1 : per_cu_chain4);
+  d->chain_grid = d->chain_grid5;
+  const int chain_max = d->chain_grid5 > d->chain_grid4 ? d->chain_grid5 : d->chain_grid4;
+  const int spill_grid = d->b1_grid > chain_max ? d->b1_grid : chain_max;
   const int spill_lanes = spill_grid * b1::kBlock;
   // path record chunks beyond the two in registers (Record): ceil(max_depth / 4) - 2 per lane
   const int chunks = (s->camera.max_depth + 3) / 4 - 2;
@@ -1202,6 +1214,11 @@ static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V
     else hipLaunchKernelGGL((rt_book1_chain_kernel<false, true>), gc, blk, bytes, st, V, d_out);
     return;
   }
+  if (d->chain_occ == 4) {
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, false, 4>), gc, blk, lds, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, false, 4>), gc, blk, 0, st, V, d_out);
+    return;
+  }
   if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, lds, st, V, d_out);
   else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, V, d_out);
 }
@@ -1231,6 +1248,15 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp) {
 static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
   const Config &cfg = d->cfg;
   if (chain_records(d, (size_t)npix, V.S.cam.spp) != 0) return -1;
+  // waves per SIMD: 5 hide more latency (headline frame 270 vs 282 ms at 4), 4 run each lane chain
+  // faster -- what a launch with few pixels per lane needs (its time is its longest chains)
+  {
+    int occ = cfg.chain_occ;
+    if (cfg.recut) occ = 4;
+    else if (occ != 4 && occ != 5) occ = (double)npix >= cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 4;
+    d->chain_occ = occ;
+    d->chain_grid = occ == 5 ? d->chain_grid5 : d->chain_grid4;
+  }
   launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
@@ -1803,7 +1829,11 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   }
   const int mode = pick_mode(d, (int64_t)d->width * d->height);
   const char *lds = d->b1_lds_bytes ? "true" : "false";
-  snprintf(buf, sizeof buf, "%s<%s>", mode == kModeChain ? "rt_book1_chain_kernel" : "rt_book1_kernel", lds);
+  if (mode == kModeChain)  // (every template argument, as rocprofv3 demangles the name: kLds, kRecut, kOcc)
+    snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %s, %d>", lds, d->cfg.recut ? "true" : "false",
+             d->cfg.recut ? 5 : d->chain_occ);
+  else
+    snprintf(buf, sizeof buf, "rt_book1_kernel<%s>", lds);
   return buf;
 }
 
