@@ -556,7 +556,8 @@ struct Config {
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int chain_occ = 0;          // chain kernel waves per SIMD: 4, 5, or 0 = by pixels per lane (below)
-  float chain_occ_px = 0.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5
+  float chain_occ_px = 0.5f;  //   auto: 5 when the launch has at least this many pixels per lane at 5
+                              //   (headline frame: 2.47 at N = 1 ... 0.31 at N = 8)
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
