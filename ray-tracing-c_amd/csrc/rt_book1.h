@@ -247,7 +247,7 @@ struct Lane {         // plain scalars: an f3 member here was kept in scratch by
   float a, tmax;      // |d|^2, closest hit so far
   float ra;           // refined reciprocal of a (div_core), hoisted per ray
   bool fast;          // a in the range where div_core == '/'
-  int32_t hit;        // sphere index or -1
+  int32_t hit;        // the hit leaf item's byte offset (as cur), or -1
   uint32_t cur;       // preorder item being visited (byte offset: index x 16)
 };
 
@@ -262,9 +262,12 @@ RT_D bool aabb_packed(float4 a, float4 b, const Lane &L, float tmin) {
   const float t0x = L.ix < 0 ? px.y : px.x, t1x = L.ix < 0 ? px.x : px.y;
   const float t0y = L.iy < 0 ? py.y : py.x, t1y = L.iy < 0 ? py.x : py.y;
   const float t0z = L.iz < 0 ? pz.y : pz.x, t1z = L.iz < 0 ? pz.x : pz.y;
-  const float lo = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);
-  const float hi = fminf(fminf(fminf(L.tmax, t1x), t1y), t1z);
-  return !(hi <= lo);
+  const float lo = fmaxf(fmaxf(fmaxf(tmin, t0x), t0y), t0z);  // (never NaN: tmin is not)
+  // hi = fminf(fminf(fminf(tmax, t1x), t1y), t1z) = fminf(tmax, m): "hi <= lo" iff "tmax <= lo" or
+  // "m <= lo" (m NaN only when all three are, and then hi = tmax).  Testing the two separately spares
+  // the canonicalisation of tmax (a loop-carried value) that fminf(tmax, ...) costs in every step.
+  const float m = fminf(fminf(t1x, t1y), t1z);
+  return !(L.tmax <= lo) & !(m <= lo);
 }
 
 // Sphere_hit (src/hittable.c:120-151) as the reference writes it: the diagnostics' yardstick for
@@ -356,7 +359,7 @@ RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L
   // the straight-line step measured 1.3x slower)
   uint32_t next = p + 16u;
   if (w & kLeaf9) {
-    sphere_test_data(q0, (int)(w & 0x7fffffffu), L, tmin);
+    sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
   } else {
     if (!aabb_packed(q0, q1, L, tmin)) next = p + (__float_as_uint(q1.z) << 4);
   }
@@ -1367,6 +1370,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // whole-wave traces would take issue slots from lanes that still make full use of them.  The
     // helper count is read at most every ~20 us per wave (a device-scope load per shading pass from
     // every sparse wave measured 25 % slower lanes: one hot line).
+    // (Letting any drained wave migrate once 70-95 % of the waves had finished measured 8 % slower
+    // at N = 8: whole-wave traces of dense waves' chains take the helpers from the sparse ones.)
     bool mig_try = false;
     if (kMode == kMigMode && V.mig_live > 0 && live < 64 && live <= V.mig_live) {
       if (!mig_ok) {
@@ -1387,15 +1392,19 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         tail = ld3(cam.background);
         path_done = true;
       } else {
-        const rt_sphere &sp = V.S.spheres[L.hit];
+        // the sphere from its leaf item (LDS): centre in q0, 1/r and the material in q1 -- the same
+        // floats as the scene's sphere record, one LDS round trip instead of a global load
+        const char *ib = (const char *)items9 + L.hit;
+        const float4 c4 = *(const float4 *)ib, h4 = *(const float4 *)(ib + (size_t)V.n_items9_alloc * sizeof(float4));
+        const uint32_t mat = __float_as_uint(h4.z);
         const f3 d = mk(L.dx, L.dy, L.dz);
         const f3 p = ray_at(mk(L.ox, L.oy, L.oz), d, L.tmax);
-        const f3 outward = scale(sub(p, ld3(sp.center)), sp.inv_radius);
+        const f3 outward = scale(sub(p, mk(c4.x, c4.y, c4.z)), h4.y);
         const bool front = dot(d, outward) < 0.0f;
         const f3 normal = front ? outward : neg(outward);
-        const FastMat &m = V.mats[sp.material];
+        const FastMat &m = V.mats[mat];
         const f3 nd = scatter(m, normal, front, d, g);
-        rec_push(V, R, (uint32_t)sp.material, glane);
+        rec_push(V, R, mat, glane);
         L.ox = p.x, L.oy = p.y, L.oz = p.z;
         L.dx = nd.x, L.dy = nd.y, L.dz = nd.z;
         depth--;
