@@ -86,7 +86,8 @@ __global__ __launch_bounds__(kBlock) void rt_render_deep_kernel(DScene S, int ro
 // Persistent Book-1 kernels (rt_book1.h): grid = resident workgroups, lanes steal work items.  The
 // chain kernel, its cost pre-pass and the lane kernel run at 5 waves per SIMD (96 VGPRs; the chain
 // kernel spills 15, none in the traversal loop: 270 ms vs 282 ms at 4 waves; with the
-// SLP vectorizer's packed f32 ops it needed 128 and spilled 65 at 5); the re-cut variant at 4 (its
+// SLP vectorizer's packed f32 ops it needed 128 and spilled 65 at 5); launches with few pixels per lane
+// (N >= 2 shares) use the 3-wave instantiation (launch_chain); the re-cut variant runs at 4 (its
 // intra-wave handoff region in LDS does not fit 5 workgroups beside the scene).
 template <bool kLds>
 __global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
@@ -555,9 +556,11 @@ struct Config {
   int recut_min = 32;      //   of chains with at least this many samples left
   float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
-  int chain_occ = 0;          // chain kernel waves per SIMD: 4, 5, or 0 = by pixels per lane (below)
-  float chain_occ_px = 0.5f;  //   auto: 5 when the launch has at least this many pixels per lane at 5
-                              //   (headline frame: 2.47 at N = 1 ... 0.31 at N = 8)
+  int chain_occ = 0;          // chain kernel waves per SIMD: 3, 4, 5, or 0 = by pixels per lane (below)
+  float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
+                              //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
+                              //   same box, N = 1 / 2 / 4 / 8: 3 waves 268 / 168 / 100 / 68.5 ms, 4 waves
+                              //   274-277 / 172-180 / 102-104 / 69-70, 5 waves 265-267 / 172-177 / 105 / 70-73)
   static Config from_env() {
     Config c;
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
@@ -643,7 +646,7 @@ struct rt_device_scene {
   void *b1_arena = nullptr;
   size_t b1_lds_bytes = 0;
   int b1_grid = 0, chain_grid = 0;  // chain_grid: the current chain launch's (one of the two below)
-  int chain_grid5 = 0, chain_grid4 = 0, chain_occ = 5;  // chain kernel grids at 5 / 4 waves per SIMD
+  int chain_grid5 = 0, chain_grid4 = 0, chain_grid3 = 0, chain_occ = 5;  // chain kernel grids at 5 / 4 / 3 waves per SIMD
   uint32_t *lpt_cost = nullptr;  // pre-pass steps per work item (W*H)
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
@@ -895,7 +898,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->b1_lds_bytes = align_up(lds ? items_bytes : 0, 16);
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
-  int per_cu = 0, per_cu_chain = 0, per_cu_chain4 = 0;
+  int per_cu = 0, per_cu_chain = 0, per_cu_chain4 = 0, per_cu_chain3 = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock,
       d->b1_lds_bytes));
@@ -910,10 +913,14 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu_chain4, lds ? (const void *)rt_book1_chain_kernel<true, false, 4> : (const void *)rt_book1_chain_kernel<false, false, 4>,
       b1::kBlock, d->b1_lds_bytes));
-  if (cfg.recut) per_cu_chain4 = per_cu_chain;  // (one instantiation, occupancy 4)
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu_chain3, lds ? (const void *)rt_book1_chain_kernel<true, false, 3> : (const void *)rt_book1_chain_kernel<false, false, 3>,
+      b1::kBlock, d->b1_lds_bytes));
+  if (cfg.recut) per_cu_chain4 = per_cu_chain3 = per_cu_chain;  // (one instantiation, occupancy 4)
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid5 = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   d->chain_grid4 = prop.multiProcessorCount * (per_cu_chain4 < 1 ? 1 : per_cu_chain4);
+  d->chain_grid3 = prop.multiProcessorCount * (per_cu_chain3 < 1 ? 1 : per_cu_chain3);
   d->chain_grid = d->chain_grid5;
   const int chain_max = d->chain_grid5 > d->chain_grid4 ? d->chain_grid5 : d->chain_grid4;
   const int spill_grid = d->b1_grid > chain_max ? d->b1_grid : chain_max;
@@ -1215,6 +1222,11 @@ static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V
     else hipLaunchKernelGGL((rt_book1_chain_kernel<false, true>), gc, blk, bytes, st, V, d_out);
     return;
   }
+  if (d->chain_occ == 3) {
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, false, 3>), gc, blk, lds, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, false, 3>), gc, blk, 0, st, V, d_out);
+    return;
+  }
   if (d->chain_occ == 4) {
     if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, false, 4>), gc, blk, lds, st, V, d_out);
     else hipLaunchKernelGGL((rt_book1_chain_kernel<false, false, 4>), gc, blk, 0, st, V, d_out);
@@ -1249,14 +1261,15 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp) {
 static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
   const Config &cfg = d->cfg;
   if (chain_records(d, (size_t)npix, V.S.cam.spp) != 0) return -1;
-  // waves per SIMD: 5 hide more latency (headline frame 270 vs 282 ms at 4), 4 run each lane chain
-  // faster -- what a launch with few pixels per lane needs (its time is its longest chains)
+  // waves per SIMD: 5 hide more latency (headline frame 266 vs 275 ms at 4), 3 run each lane chain
+  // faster with no spills at all (168 VGPRs) -- what a launch with few pixels per lane needs (its time
+  // is its longest chains)
   {
     int occ = cfg.chain_occ;
     if (cfg.recut) occ = 4;
-    else if (occ != 4 && occ != 5) occ = (double)npix >= cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 4;
+    else if (occ < 3 || occ > 5) occ = (double)npix >= cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 3;
     d->chain_occ = occ;
-    d->chain_grid = occ == 5 ? d->chain_grid5 : d->chain_grid4;
+    d->chain_grid = occ == 5 ? d->chain_grid5 : occ == 4 ? d->chain_grid4 : d->chain_grid3;
   }
   launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());

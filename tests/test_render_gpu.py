@@ -221,7 +221,7 @@ CHAIN = {"RT_MODE": "chain", "RT_LPT_SPP": "1", "RT_CHAIN_MIN_SEG": "4"}
     {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_MB": "1"},       # out of records: pixels stay whole
     {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BOOK1_LDS": "0"},      # global-memory scene, lanes only
     {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BF": "0", "RT_CHAIN_KMAX": "2"},
-    {**CHAIN, "RT_CHAIN_OCC": "4"}, {**CHAIN, "RT_CHAIN_OCC": "5"},  # both chain kernel occupancies
+    {**CHAIN, "RT_CHAIN_OCC": "3"}, {**CHAIN, "RT_CHAIN_OCC": "4"}, {**CHAIN, "RT_CHAIN_OCC": "5"},  # every occupancy
 ])
 @pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
 def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
@@ -249,7 +249,7 @@ def test_book1_deep_paths_spill(monkeypatch):
 
 @pytest.mark.parametrize("env", [{}, {"RT_CHAIN_BETA": "0.002"}, {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_KMAX": "64"},
                                  {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},
-                                 {"RT_CHAIN_OCC": "4"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"}])
+                                 {"RT_CHAIN_OCC": "3"}, {"RT_CHAIN_OCC": "4"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"}])
 def test_chain_render_north_star_scene(manifest, env, monkeypatch):
     """Chain render (rt_book1.h: ChainPx) forced on the Book-1 final scene at full size: pixel
     streams cut into segments, chains coupling on equal stream offsets, the fold and the
