@@ -346,7 +346,7 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
   const char *why = "not a JPEG file";
   if (!j) return NULL;
   const uint8_t *p = buf, *end = buf + len;
-  int have_frame = 0;
+  int have_frame = 0, decoded = 0; /* decoded: bit k set once component k's scan is done */
   if (len < 4 || p[0] != 0xff || p[1] != 0xd8) goto fail;
   p += 2;
   for (;;) {
@@ -357,8 +357,9 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
       goto fail;
     }
     const int m = *p++;
-    if (m == 0xd9) {
-      why = "JPEG without a scan";
+    if (m == 0xd9) { /* EOI: an image whose components came in separate scans is complete here */
+      if (have_frame && decoded == (1 << j->nc) - 1) break;
+      why = decoded ? "JPEG ends before every component was scanned" : "JPEG without a scan";
       goto fail;
     }
     if (m >= 0xd0 && m <= 0xd7) continue;
@@ -369,11 +370,13 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
       why = "corrupt JPEG segment";
       goto fail;
     }
+    /* every read below stays inside [seg, next): tables and headers are checked against L first */
+    why = "corrupt JPEG segment";
     if (m == 0xdb) { /* DQT */
       for (const uint8_t *q = seg; q < next;) {
         const int pq = *q >> 4, tq = *q & 15;
         q++;
-        if (tq > 3) goto fail;
+        if (tq > 3 || pq > 1 || q + (pq ? 128 : 64) > next) goto fail;
         for (int k = 0; k < 64; k++) j->q[tq][k] = (uint16_t)(pq ? rd16(q + 2 * k) : q[k]);
         q += pq ? 128 : 64;
       }
@@ -381,12 +384,12 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
       for (const uint8_t *q = seg; q < next;) {
         const int tc = *q >> 4, th = *q & 15;
         q++;
-        if (tc > 1 || th > 3) goto fail;
+        if (tc > 1 || th > 3 || q + 16 > next) goto fail;
         Huff *t = tc ? &j->ha[th] : &j->hd[th];
         int n = 0;
         for (int k = 0; k < 16; k++) n += (t->bits[k] = q[k]);
         q += 16;
-        if (n > 256) goto fail;
+        if (n > 256 || q + n > next) goto fail;
         t->n = n;
         memcpy(t->vals, q, (size_t)n);
         q += n;
@@ -396,6 +399,7 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
         }
       }
     } else if (m == 0xdd) { /* DRI */
+      if (L < 4) goto fail;
       j->restart = rd16(seg);
     } else if (m == 0xe0 && L >= 7 && !memcmp(seg, "JFIF", 5)) { /* APP0 JFIF: YCbCr */
       j->jfif = 1;
@@ -403,6 +407,7 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
       j->adobe = 1;
       j->transform = seg[11];
     } else if (m == 0xc0 || m == 0xc1) { /* SOF0 / SOF1: baseline, extended Huffman */
+      if (have_frame || L < 8) goto fail; /* (one frame per image) */
       if (seg[0] != 8) {
         why = "JPEG with other than 8-bit samples";
         goto fail;
@@ -414,6 +419,7 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
         why = "unsupported JPEG frame (size or component count)";
         goto fail;
       }
+      if (L < 8 + 3 * j->nc) goto fail;
       j->hmax = j->vmax = 1;
       for (int k = 0; k < j->nc; k++) {
         Comp *c = &j->c[k];
@@ -425,23 +431,32 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
         if (c->h > j->hmax) j->hmax = c->h;
         if (c->v > j->vmax) j->vmax = c->v;
       }
+      /* the upsamplers need whole ratios (stb_image rejects the others: "bad H" / "bad V") */
+      for (int k = 0; k < j->nc; k++)
+        if (j->hmax % j->c[k].h || j->vmax % j->c[k].v) {
+          why = "unsupported JPEG sampling factors (not whole ratios)";
+          goto fail;
+        }
       const int mw = (j->w + 8 * j->hmax - 1) / (8 * j->hmax), mh = (j->h + 8 * j->vmax - 1) / (8 * j->vmax);
       for (int k = 0; k < j->nc; k++) {
         Comp *c = &j->c[k];
         c->bw = mw * c->h;
         c->bh = mh * c->v;
         c->data = calloc((size_t)c->bw * 8 * c->bh * 8, 1);
-        if (!c->data) goto fail;
+        if (!c->data) {
+          why = "out of memory";
+          goto fail;
+        }
       }
       have_frame = 1;
     } else if (m >= 0xc2 && m <= 0xcf && m != 0xc4 && m != 0xc8 && m != 0xcc) {
       why = "unsupported JPEG coding (progressive, lossless or arithmetic)";
       goto fail;
     } else if (m == 0xda) { /* SOS */
-      if (!have_frame) goto fail;
+      if (!have_frame || L < 3) goto fail;
       const int ns = seg[0];
       int order[3];
-      if (ns < 1 || ns > j->nc) goto fail;
+      if (ns < 1 || ns > j->nc || L < 6 + 2 * ns) goto fail;
       for (int q = 0; q < ns; q++) {
         const int id = seg[1 + 2 * q];
         int k = 0;
@@ -460,7 +475,8 @@ uint8_t *rt_jpeg_decode(const uint8_t *buf, size_t len, int *width, int *height,
         why = "corrupt JPEG entropy-coded data";
         goto fail;
       }
-      if (ns == j->nc) break; /* (one interleaved scan holds the whole image) */
+      for (int q = 0; q < ns; q++) decoded |= 1 << order[q];
+      if (decoded == (1 << j->nc) - 1) break; /* every component decoded: the image is complete */
       /* non-interleaved scans follow one another: resume the segment walk at the marker after this scan */
       p = j->marker ? j->p - 2 : j->p;
       while (p + 1 < end && !(p[0] == 0xff && p[1] != 0 && p[1] != 0xff && !(p[1] >= 0xd0 && p[1] <= 0xd7))) p++;

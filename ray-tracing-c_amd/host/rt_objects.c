@@ -498,8 +498,14 @@ void Image_init(Image *self, char *filename) {
     for (;;) {
       if (len == cap) {
         cap = cap ? 2 * cap : 1 << 20;
-        buf = realloc(buf, cap);
-        if (!buf) break;
+        uint8_t *grown = realloc(buf, cap);
+        if (!grown) {  /* (the block read so far is freed, the failure named) */
+          free(buf);
+          buf = NULL;
+          snprintf(why, sizeof why, "out of memory reading the file");
+          break;
+        }
+        buf = grown;
       }
       const size_t got = fread(buf + len, 1, cap - len, f);
       len += got;

@@ -246,3 +246,84 @@ def test_preset_substitute_picture_is_opt_in(tmp_path, monkeypatch):
     sc = rtc.Scene.preset(7, 40, 1, 1, substitute_earth=True)
     assert _flat_image(sc).shape == (512, 1024, 3)
     assert os.getcwd() == str(tmp_path)
+
+
+def _jpeg_fuzz_exe():
+    exe = os.path.join(ROOT, "tests", "native", "bin", "jpeg_fuzz")
+    src = [os.path.join(ROOT, "tests", "native", "jpeg_fuzz.c"), os.path.join(ROOT, "ray-tracing-c_amd", "host", "rt_jpeg.c")]
+    if not os.path.exists(exe) or any(os.path.getmtime(s) > os.path.getmtime(exe) for s in src):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "native"), "bin/jpeg_fuzz"], check=True,
+                       capture_output=True)
+    return exe
+
+
+def test_jpeg_decoder_survives_truncated_and_corrupted_files(tmp_path):
+    """every table / header read of host/rt_jpeg.c is bounded by its segment.  The decoder,
+    built with AddressSanitizer + UBSan (tests/native/jpeg_fuzz), runs over truncations at every byte of
+    the headers and every 9th byte after them, and over single-byte corruptions of the headers; each
+    file must decode or be rejected -- never read out of bounds (ASan exits non-zero)."""
+    import jpeg_tools
+
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 255, (20, 27, 3), dtype=np.uint8)
+    files = []
+    for name, data in (("il", jpeg_tools.encode(img, True)), ("nil", jpeg_tools.encode(img, False)),
+                       ("grey", jpeg_tools.encode(img[..., 0], False))):
+        sos = data.index(b"\xff\xda")
+        for n in list(range(0, sos + 16)) + list(range(sos + 16, len(data), 9)):
+            files.append((f"{name}_t{n}", data[:n]))
+        for n in range(2, sos + 12):
+            for v in (0x00, 0xFF, data[n] ^ 0x5A, 0x01):
+                files.append((f"{name}_c{n}_{v}", data[:n] + bytes([v]) + data[n + 1:]))
+    # segments whose length field is shorter than the table / header they announce, at the end of the
+    # file: the old walk read the announced bytes past the buffer
+    il = jpeg_tools.encode(img, True)
+    frame = il[:il.index(b"\xff\xc4")]  # SOI, APP0, DQT, SOF0
+    for k, tail in enumerate((b"\xff\xdb\x00\x03\x00", b"\xff\xc4\x00\x03\x00", b"\xff\xdd\x00\x02",
+                              b"\xff\xc0\x00\x03\x08", b"\xff\xc4\x00\x13\x00" + bytes([0] * 15) + b"\x09")):
+        files.append((f"short{k}", il[:2] + tail))
+    files.append(("short_sos", frame + b"\xff\xda\x00\x03\x03"))
+    # a frame whose sampling factors are not whole ratios (h 3 vs 2): rejected, as stb_image does
+    bad = bytearray(jpeg_tools.encode(img, True))
+    sof = bad.index(b"\xff\xc0")
+    bad[sof + 11], bad[sof + 14] = 0x31, 0x21
+    files.append(("ratio", bytes(bad)))
+    paths = []
+    for name, data in files:
+        p = tmp_path / f"{name}.jpg"
+        p.write_bytes(data)
+        paths.append(str(p))
+    exe = _jpeg_fuzz_exe()
+    for k in range(0, len(paths), 500):
+        r = subprocess.run([exe] + paths[k:k + 500], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    r = subprocess.run([exe, paths[-1]], capture_output=True, text=True, timeout=60)
+    assert r.stdout.startswith("err") and "sampling" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("grey", [False, True])
+def test_image_new_decodes_non_interleaved_jpeg(tmp_path, grey):
+    """a baseline JPEG whose components come in separate scans (T.81 §A.2.2; Pillow never
+    writes one) decodes to exactly the pixels of the same coefficients in one interleaved scan, and
+    agrees with Pillow's libjpeg within the usual IDCT / colour rounding."""
+    import jpeg_tools
+
+    rng = np.random.default_rng(11)
+    h, w = 45, 70
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = np.stack([xx * 255 // (w - 1), yy * 255 // (h - 1), (xx ^ yy) & 255], -1)
+    img = (img + rng.integers(-15, 15, img.shape)).clip(0, 255).astype(np.uint8)
+    if grey:
+        img = img[..., 1]
+    got = {}
+    for layout in (True, False):
+        d = tmp_path / ("il" if layout else "nil")
+        d.mkdir()
+        (d / "earthmap.jpg").write_bytes(jpeg_tools.encode(img, layout))
+        got[layout] = _flat_image(rtc.Scene.preset(3, 40, 1, 1, image_dir=str(d))).astype(int)
+    assert np.array_equal(got[True], got[False])
+    PIL = pytest.importorskip("PIL.Image")
+    ref = np.asarray(PIL.open(tmp_path / "nil" / "earthmap.jpg").convert("RGB")).astype(int)
+    assert ref.shape == got[False].shape
+    diff = np.abs(ref - got[False])
+    assert diff.max() <= 3 and diff.mean() < 0.5, (diff.max(), diff.mean())
