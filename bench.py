@@ -323,6 +323,7 @@ def main():
             "cpu_baseline": base,
             "end_to_end": e2e,
             "parity": parity,
+            "box": rtc.box_identity(local),
         }
         if share:
             line["rehearsal"] = "RT_BENCH_SHARE_DEVICE: ranks share GPUs over gloo; timings contended, not a result"

@@ -66,33 +66,9 @@ struct ChainPx {       // 32 B per pixel of a chain launch (chain_plan_kernel)
   uint32_t end0;       // segment k's end word at ch_seg[end0 + k]
   uint32_t check;      // a segment >= 1 looks for the pixel's end once it holds this many records
   uint32_t cap_last;   // records of the last segment (it takes whatever remains of the stream)
-  uint32_t kd;         // run-time re-cut (RecutReq): dynamic segments published (low 8 bits; atomic);
-                       // bit 8 while one is being published
+  uint32_t pad;
 };
-// Run-time re-cut.  Once a launch's work items are all handed out (its tail), a chain with much of
-// its stream left asks for a cut (RecutReq): a lane that found no item left (or an idle helper wave)
-// inserts a dynamic segment t right after the chain's segment k, at an offset ahead of it -- a fraction
-// of the draws between k's position and the start of k's successor (for a last segment: of the
-// stream's remaining true samples times the chain's draws per sample) -- with a record list of its
-// own, and runs it.  Segment k, watching its successor word since it asked, couples into t exactly as
-// into a planned successor, and t couples into k's old successor.  Segments stay ordered by start
-// offset (links point forward in offset), so the fold is unchanged.  Per segment slot end0 + t
-// (t < K + kDynMax; the planner reserves the slots): the end word ch_seg, and SegDyn: a dynamic
-// segment's start, record base and capacity, and for every segment its successor once a cut changed it.
-constexpr uint32_t kDynMax = 8;
 constexpr uint32_t kNone = 0xffu;  // no successor
-struct SegDyn {        // 16 B per segment slot
-  uint32_t start, base, cap;  // a dynamic segment: stream offset, first record, records
-  uint32_t next;              // 0: the planned successor (t + 1 < K ? t + 1 : none); else successor + 1
-};
-struct RecutReq {      // 32 B: a chain asking to be cut (pushed by its lane / helper wave)
-  uint32_t pix, seg;
-  uint32_t x_new;      // the new segment's start offset
-  uint32_t next;       // k's successor when it asked (the cut is stale if that changed)
-  uint32_t cap;        // records for the new segment
-  uint32_t ready;      // the launch's epoch, written last (release)
-  uint32_t pad[2];
-};
 struct ChainCont {     // 32 B: a continuation item -- the true chain from an exact position
   uint32_t pix, o, s, pad;
   float acc[4];
@@ -112,10 +88,9 @@ struct ChainCont {     // 32 B: a continuation item -- the true chain from an ex
 // would swamp that memory channel and slow every working lane (measured: +30 % at N = 8).
 // After the launch, chain_check_kernel compares [0] with the launch's item count: a launch that
 // finished fewer items than it was given is reported through the scene's status word.
-// Words [32, 64) (their own line): the re-cut request queue's push / pop indices.
 constexpr int kMigBoxes = 64, kMigBoxWords = 32;
 enum : int {
-  kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigRqPush = 32, kMigRqPop = 33, kMigBox0 = 64,
+  kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigBox0 = 64,
   kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3
 };
 constexpr int kMigWords = kMigBox0 + kMigBoxes * kMigBoxWords;
@@ -156,6 +131,7 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
+  int32_t leaf_min;          // trav_step_v9: a leaf's sphere test waits until this many stepping lanes are at leaves
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
@@ -192,35 +168,13 @@ struct Book1View {
                          // resident made N = 8 shares 20 % slower, however rarely they polled)
   uint32_t mig_drop;     // fault injection (tests only): helpers drop this many popped items unrun
   uint64_t mig_wait;     // a helper idle this long (wall_clock64 ticks, 100 MHz) offers to leave
-  // run-time re-cut (RecutReq); rq == null: off
-  RecutReq *rq;
-  uint32_t rq_cap;
-  SegDyn *ch_sd;         // per segment slot [end0 + t]
-  unsigned long long *rec_count;  // records allocated (the planner's counter; cuts allocate from it too)
-  const uint32_t *rec_filled;     // records whose end word holds kRecFill (chain_fill_kernel): cuts stay below
-  uint32_t recut_min;    // a chain asks when at least this many of its samples remain
-  float recut_frac;      // the cut keeps this share of the chain's remaining draws on the chain
-  uint32_t recut_slack;  // records of a dynamic segment: 2 x its share of samples + this
-  uint32_t *recut_stats; // diagnostics (accumulated per scene): [0] cuts published, [1] requests declined
-  int32_t recut_lanes;   // chain launches: a lane cuts its chain for an idle lane of its own wave
 };
 
-// ---------------------------------------------------------------- chain segments (planned + dynamic)
-RT_D uint32_t ld_sd(const uint32_t &w) { return ld_rel(&w); }
-RT_D uint32_t seg_start(const Book1View &V, const ChainPx &P, uint32_t t) {
-  return t < P.K ? t * P.seg_len : ld_sd(V.ch_sd[P.end0 + t].start);
-}
-RT_D uint32_t seg_cap(const Book1View &V, const ChainPx &P, uint32_t k) {
-  return k + 1u < P.K ? P.cap : k + 1u == P.K ? P.cap_last : ld_sd(V.ch_sd[P.end0 + k].cap);
-}
-RT_D uint32_t rec_index(const Book1View &V, const ChainPx &P, uint32_t t, uint32_t c) {
-  return t < P.K ? P.rec0 + (t - 1u) * P.cap + c : ld_sd(V.ch_sd[P.end0 + t].base) + c;
-}
-RT_D uint32_t seg_next(const Book1View &V, const ChainPx &P, uint32_t t) {  // successor segment, or kNone
-  const uint32_t v = V.ch_sd ? ld_acq(&V.ch_sd[P.end0 + t].next) : 0u;
-  if (v) return v - 1u;
-  return t + 1u < P.K ? t + 1u : kNone;
-}
+// ---------------------------------------------------------------- chain segments
+RT_D uint32_t seg_start(const ChainPx &P, uint32_t t) { return t * P.seg_len; }
+RT_D uint32_t seg_cap(const ChainPx &P, uint32_t k) { return k + 1u < P.K ? P.cap : P.cap_last; }
+RT_D uint32_t rec_index(const ChainPx &P, uint32_t t, uint32_t c) { return P.rec0 + (t - 1u) * P.cap + c; }
+RT_D uint32_t seg_next(const ChainPx &P, uint32_t t) { return t + 1u < P.K ? t + 1u : kNone; }  // or kNone
 
 // ---------------------------------------------------------------- pixel output
 // quantize one pixel (src/raytracing.c:127-131): mean, gamma 2, clamp-macro semantics, truncate
@@ -342,8 +296,14 @@ RT_D float4 it_q0(const float4 *items, uint32_t p) { return items[p]; }
 RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint32_t)na + p]; }
 
 // L.cur, na16 and n16 are byte offsets (item index x 16): na16 = 16 V.n_items9_alloc, n16 = 16 V.n_items9
-// (hoisted by the caller, in VGPRs) -- the step then needs no index scaling
-RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L, float tmin) {
+// (hoisted by the caller, in VGPRs) -- the step then needs no index scaling.
+// Leaves wait for company: a lane at a leaf runs its sphere test only once at least leaf_min of the
+// stepping lanes sit at leaves (or no lane sits at a node); until then it stays on its item while
+// the node lanes go on.  Leaves are ~6 % of the scan's items (7.2 sphere tests per 111 boxes a ray,
+// SURVEY §8d), so in an if-if step some lane of the wave is at a leaf nearly every time and the
+// sphere block ran for one or two lanes; a lane's own sequence of items is unchanged (exact).
+// The caller calls this with exec = the stepping lanes (the ballots count those).
+RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L, float tmin, int leaf_min = 1) {
   const uint32_t p = L.cur;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const char *base = (const char *)items;
@@ -358,8 +318,15 @@ RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L
   // (branches, not both tests straight-line for every lane: a wave's lanes are mostly at one kind --
   // the straight-line step measured 1.3x slower)
   uint32_t next = p + 16u;
-  if (w & kLeaf9) {
-    sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
+  const bool leaf = (w & kLeaf9) != 0u;
+  bool do_leaf = true;
+  if (leaf_min > 1) {  // (wave-uniform)
+    const uint64_t lm = __ballot(leaf), all = __ballot(true);
+    do_leaf = lm == all || (int)__popcll(lm) >= leaf_min;
+  }
+  if (leaf) {
+    if (do_leaf) sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
+    else next = p;  // waits at its leaf
   } else {
     if (!aabb_packed(q0, q1, L, tmin)) next = p + (__float_as_uint(q1.z) << 4);
   }
@@ -599,30 +566,21 @@ RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, f
 }
 
 // ---------------------------------------------------------------- chain protocol (kMode 2)
-// Coupling cursor: successor segment t << 24 | flags | record c.  kWatch: the chain has asked for a cut
-// and reads its successor word until a new successor shows up; kNoAsk: it never asks (too little left).
-constexpr uint32_t kWatch = 0x800000u, kNoAsk = 0x400000u, kCurRec = 0x3fffffu;
+// Coupling cursor: successor segment t << 24 | record c.
+constexpr uint32_t kCurRec = 0xffffffu;
 
 // Coupling scan of chain k at its sample boundary x: does a successor record start at x?  tc = the
 // cursor, st = the start offset of its record.  Returns true when coupled (tc then names the record
 // that starts at x).  Bounded work per call; a record not yet written, or a successor still running
 // past its last record, is looked at again next time.
 RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t x, uint32_t &tc, uint32_t &st) {
-  if (tc & kWatch) {  // asked for a cut: a new successor?  (switch only if it starts ahead of this chain)
-    const uint32_t n = seg_next(V, P, k);
-    if (n != (tc >> 24)) {
-      const uint32_t sn = seg_start(V, P, n);
-      if (sn > x) tc = n << 24, st = sn;
-      else tc &= ~kWatch;  // (it landed behind this chain: ignore it, it couples into the old successor)
-    }
-  }
   for (int it = 0; it < 24; it++) {
     const uint32_t t = tc >> 24, c = tc & kCurRec;
-    if (t >= P.K + kDynMax) return false;  // no successor (kNoTarget)
+    if (t >= P.K) return false;  // no successor (kNoTarget)
     if (st > x) return false;  // the successor's next sample starts beyond x
     if (st == x) return true;
-    if (c < seg_cap(V, P, t)) {  // st < x: step over record c
-      const uint32_t e = ld_rel(&V.ch_end[rec_index(V, P, t, c)]);
+    if (c < seg_cap(P, t)) {  // st < x: step over record c
+      const uint32_t e = ld_rel(&V.ch_end[rec_index(P, t, c)]);
       if (e != kRecFill) {
         st = e;
         tc = (tc & ~kCurRec) | (c + 1u);
@@ -633,20 +591,20 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_
     const uint64_t w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded) || c < end_n(w)) return false;  // running, or its record c still in flight
     if (w & kEndNoLink) {
-      tc = kNoTarget | (tc & kNoAsk);  // it ended without a link: nothing to couple with beyond it
+      tc = kNoTarget;  // it ended without a link: nothing to couple with beyond it
       return false;
     }
     const uint32_t t2 = end_t(w), c2 = end_c(w);
-    if (t2 == t || t2 >= P.K + kDynMax) {  // (never: links point forward)
-      tc = kNoTarget | (tc & kNoAsk);
+    if (t2 <= t || t2 >= P.K) {  // (never: links point forward)
+      tc = kNoTarget;
       return false;
     }
-    uint32_t s2 = seg_start(V, P, t2);
+    uint32_t s2 = seg_start(P, t2);
     if (c2 > 0) {
-      s2 = ld_rel(&V.ch_end[rec_index(V, P, t2, c2 - 1u)]);
+      s2 = ld_rel(&V.ch_end[rec_index(P, t2, c2 - 1u)]);
       if (s2 == kRecFill) return false;
     }
-    tc = (t2 << 24) | (tc & kNoAsk) | c2;  // (a followed link ends any watch: the cut, if one comes, is behind)
+    tc = (t2 << 24) | c2;
     st = s2;
   }
   return false;
@@ -660,37 +618,14 @@ RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint
   if (!(w & kEndEnded)) return false;
   if (w & kEndNoLink) return true;  // segment 0 completed the pixel
   uint32_t total = end_n(w), t = end_t(w), c = end_c(w);
-  const uint32_t sk = seg_start(V, P, k);
-  for (uint32_t it = 0; it < P.K + kDynMax; it++) {
+  for (uint32_t it = 0; it < P.K; it++) {
     if (t == k) return total + (n - c) >= spp;
-    if (seg_start(V, P, t) > sk) return true;  // the true chain skips this chain
+    if (t > k) return true;  // the true chain skips this chain
     w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded)) return false;
     if (w & kEndNoLink) return true;  // the true chain ends (or breaks) before this chain
     total += end_n(w) - c;
     if (total >= spp) return true;
-    t = end_t(w), c = end_c(w);
-  }
-  return false;
-}
-
-// The true samples the links cover before chain k's link point (record c_at of k), when every chain
-// before k has ended and the true chain reaches k; false otherwise (undecided, or k is not needed).
-RT_D bool chain_covered(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t &total, uint32_t &c_at) {
-  uint64_t w = ld_rel64(&V.ch_seg[P.end0]);
-  if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
-  total = end_n(w);
-  uint32_t t = end_t(w), c = end_c(w);
-  const uint32_t sk = seg_start(V, P, k);
-  for (uint32_t it = 0; it < P.K + kDynMax; it++) {
-    if (t == k) {
-      c_at = c;
-      return true;
-    }
-    if (seg_start(V, P, t) > sk) return false;
-    w = ld_rel64(&V.ch_seg[P.end0 + t]);
-    if (!(w & kEndEnded) || (w & kEndNoLink)) return false;
-    total += end_n(w) - c;
     t = end_t(w), c = end_c(w);
   }
   return false;
@@ -733,18 +668,18 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
     }
     return true;
   }
-  if (k > 0 && s >= seg_cap(V, P, k)) {  // the list is full
+  if (k > 0 && s >= seg_cap(P, k)) {  // the list is full
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
   if (chain_couple(V, P, k, x, tc, st)) {
     if (writer) {
       if (k == 0) V.ch_acc0[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-      st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc & ~(kWatch | kNoAsk)));
+      st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc));
     }
     return true;
   }
-  if (k > 0 && s >= (k < P.K ? P.check : 0u) && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
+  if (k > 0 && s >= P.check && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
@@ -754,7 +689,7 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
 // Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it).
 RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, f3 col, uint32_t x_end) {
   const ChainPx &P = V.ch_px[pix];
-  const uint32_t at = rec_index(V, P, k, c);
+  const uint32_t at = rec_index(P, k, c);
   V.ch_col[at] = make_float4(col.x, col.y, col.z, u2f(x_end));
   st_rel(&V.ch_end[at], x_end);
 }
@@ -762,161 +697,10 @@ RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, 
 // A chain's start: stream position, and its coupling cursor on its successor.
 RT_D void chain_start(const Book1View &V, uint32_t pix, uint32_t seg, Pcg32 &g, uint32_t &tc, uint32_t &st) {
   const ChainPx &P = V.ch_px[pix];
-  g.skip(seg_start(V, P, seg));
-  const uint32_t n = seg_next(V, P, seg);
+  g.skip(seg_start(P, seg));
+  const uint32_t n = seg_next(P, seg);
   tc = n << 24;  // (kNone << 24 == kNoTarget)
-  st = n == kNone ? 0u : seg_start(V, P, n);
-}
-// A dynamic segment (a cut): not one of the launch's work items.
-RT_D bool seg_dynamic(const Book1View &V, uint32_t pix, uint32_t seg) {
-  return !(seg & kItemUnsplit) && seg >= V.ch_px[pix].K;
-}
-
-// ---------------------------------------------------------------- run-time re-cut (RecutReq)
-// Wave helpers that also compile for the host-side protocol simulator (tests/native/chain_sim.cpp),
-// where a "wave" is one thread.
-RT_D uint32_t wv_lane() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__lane_id();
-#else
-  return 0u;
-#endif
-}
-RT_D uint32_t wv_first(uint32_t v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-#else
-  return v;
-#endif
-}
-RT_D uint32_t at_add(uint32_t *p, uint32_t v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-RT_D bool at_cas(uint32_t *p, uint32_t expect, uint32_t v) {
-  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// True samples the pixel still needs beyond chain k's s records, once the links before k are decided
-// (else kLeftUnknown).
-constexpr uint32_t kLeftUnknown = 0xffffffffu;
-RT_D uint32_t recut_left(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t s) {
-  uint32_t total = 0u, c_at = 0u;
-  if (!chain_covered(V, P, k, total, c_at)) return kLeftUnknown;
-  const uint32_t mine = s > c_at ? s - c_at : 0u;
-  const uint32_t spp = (uint32_t)V.S.cam.spp;
-  return total + mine < spp ? spp - total - mine : 0u;
-}
-
-// Chain k of pixel pix, at stream offset x with s samples (segment 0) / records (k >= 1) taken, in the
-// launch's tail: is a cut worth it?  The cut point is a fraction of the draws left before k's successor
-// (a last segment, or one stuck past its successor: of the pixel's remaining true samples times k's
-// draws per sample) ahead of x.  Fills r and returns true; sets kNoAsk when too little is left.
-RT_D bool recut_plan(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, uint32_t &tc, RecutReq &r) {
-  if (tc & (kWatch | kNoAsk) || (k & kItemUnsplit)) return false;
-  const ChainPx P = V.ch_px[pix];
-  const uint32_t x0 = seg_start(V, P, k);
-  if (s < 4u || x <= x0) return false;
-  const float per = (float)(x - x0) / (float)s;  // k's draws per sample
-  const uint32_t n = seg_next(V, P, k);
-  float draws;  // the draws k still has to run
-  bool to_end = n == kNone;
-  if (!to_end) {
-    const uint32_t sn = seg_start(V, P, n);
-    if (sn > x) {
-      draws = (float)(sn - x);
-    } else if ((float)(x - sn) < 16.0f * per) {
-      return false;  // coupling into n normally takes a few samples past its start: ask later
-    } else {
-      // past n's start without coupling: n's chain may never meet this one (a parity trap: one odd
-      // draw count flips the true chain onto odd offsets, where an even-started segment never lands),
-      // so this chain may have to run to the pixel's end -- a cut at its own parity shares that out
-      to_end = true;
-    }
-  }
-  if (to_end) {
-    const uint32_t left = recut_left(V, P, k, s);
-    if (left == kLeftUnknown) return false;  // (asks again later)
-    draws = (float)left * per;
-  }
-  const float samples = draws / per;
-  if (samples < (float)V.recut_min) {
-    if (!to_end || n == kNone) tc |= kNoAsk;  // (what is left only shrinks)
-    return false;
-  }
-  const uint32_t dx = ((uint32_t)(V.recut_frac * draws) + 1u) & ~1u;
-  const uint32_t x_new = x + (dx > 2u ? dx : 2u);
-  if (x_new >= 0x3fffffffu) return false;
-  r.pix = pix, r.seg = k, r.x_new = x_new, r.next = n;
-  // (as many records as a planned last segment: a list that fills ends its chain unlinked, and the
-  // pixel then needs a continuation launch)
-  r.cap = (uint32_t)V.S.cam.spp + V.recut_slack;
-  return true;
-}
-
-// Ask the helper waves (a chain a helper runs): enqueue the cut (one writer lane), watch the successor.
-RT_D void recut_ask(const Book1View &V, uint32_t pix, uint32_t k, uint32_t x, uint32_t s, bool writer, uint32_t &tc) {
-  RecutReq r;
-  if (!recut_plan(V, pix, k, x, s, tc, r)) return;
-  if (writer) {
-    const uint32_t idx = at_add(&V.mig[kMigRqPush], 1u);
-    if (idx < V.rq_cap) {
-      RecutReq &q = V.rq[idx];
-      q.pix = r.pix, q.seg = r.seg, q.x_new = r.x_new, q.next = r.next, q.cap = r.cap;
-      __hip_atomic_store(&q.ready, V.mig_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  tc |= kWatch;
-}
-
-// Publish the cut a request asks for (one thread).  Returns the new segment t >= 1, or 0 when the
-// request is stale (k has ended, or was cut already), the pixel has no dynamic slot left or records
-// run out.  Order: the new slot's words, then k's successor word, then the count (release each).
-RT_D uint32_t recut_publish(const Book1View &V, const RecutReq &r) {
-  const ChainPx P = V.ch_px[r.pix];
-  uint32_t *kdp = (uint32_t *)&V.ch_px[r.pix].kd;
-  const uint32_t kd = ld_acq(kdp);
-  const uint32_t t = P.K + (kd & 0xffu);
-  uint32_t ok = 0u;
-  if (!(kd & 0x100u) && t < P.K + kDynMax && t < (uint32_t)kMaxSeg &&
-      !(ld_rel64(&V.ch_seg[P.end0 + r.seg]) & kEndEnded) && seg_next(V, P, r.seg) == r.next &&
-      at_cas(kdp, kd, kd | 0x100u)) {  // lock the pixel's slots
-    const unsigned long long b =
-        __hip_atomic_fetch_add(V.rec_count, (unsigned long long)r.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (b + r.cap <= (unsigned long long)ld_rel(V.rec_filled)) {
-      SegDyn &d = V.ch_sd[P.end0 + t];
-      st_rel(&d.start, r.x_new);
-      st_rel(&d.base, (uint32_t)b);
-      st_rel(&d.cap, r.cap);
-      st_rel(&d.next, r.next + 1u);  // (kNone + 1: none)
-      st_rel64(&V.ch_seg[P.end0 + t], 0ull);
-      __hip_atomic_store(&V.ch_sd[P.end0 + r.seg].next, t + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      ok = t;
-    }
-    __hip_atomic_store(kdp, (kd & 0xffu) + (ok ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // unlock
-  }
-  if (V.recut_stats && ok) at_add(&V.recut_stats[0], 1u);  // (declines are not counted: one hot word)
-  return ok;
-}
-
-// Take the next request (one thread): its index, or -1 when the queue is empty.
-RT_D int recut_pop(const Book1View &V) {
-  for (int tries = 0; tries < 4; tries++) {
-    const uint32_t p = ld_rel(&V.mig[kMigRqPop]);
-    uint32_t q = ld_rel(&V.mig[kMigRqPush]);
-    q = q < V.rq_cap ? q : V.rq_cap;
-    if (p >= q) return -1;
-    if (at_cas(&V.mig[kMigRqPop], p, p + 1u)) {
-      const RecutReq *rp = &V.rq[p];
-      while (__hip_atomic_load(&rp->ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != V.mig_epoch) {
-#if defined(__HIP_DEVICE_COMPILE__)
-        __builtin_amdgcn_s_sleep(1);
-#endif
-      }
-      return (int)p;
-    }
-  }
-  return -1;
+  st = n == kNone ? 0u : seg_start(P, n);
 }
 
 // ---------------------------------------------------------------- whole-wave work items
@@ -924,11 +708,9 @@ RT_D int recut_pop(const Book1View &V) {
 // values and runs the same shading), and each ray is traced by the wave (bf_candidate + bf_verify,
 // or the exact scan).  The item is a whole pixel (kMode 0: its samples in order), or a chain
 // (kMode 2: segment / unsplit pixel, with the same boundary protocol as a lane).
-// tail: the launch's work items are all handed out (a helper runs this item): the chain may ask for a
-// cut (recut_ask); whole-wave items at the launch's start never do.
 template <int kMode>
 RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix, uint32_t seg,
-                           uint8_t *__restrict__ out, const MigRec *res = nullptr, bool tail = false) {
+                           uint8_t *__restrict__ out, const MigRec *res = nullptr) {
   const rt_camera &cam = V.S.cam;
   const int W = cam.width;
   const int jj = (int)(pix / W);
@@ -958,10 +740,6 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
       if (__builtin_amdgcn_readfirstlane((int)done)) break;
-      if (V.rq && tail && (s & 3u) == 0u) {  // the launch's tail: a long chain asks for a cut
-        recut_ask(V, (uint32_t)pix, seg, g.n, s, lane0, tc);
-        tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
-      }
     } else if (s == (uint32_t)cam.spp) {
       break;
     }
@@ -1113,57 +891,23 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
       MigRec r = *q;
       r.pix = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.pix);
       r.seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.seg);
-      // (fault injection, tests only: drop the item unrun and uncounted -- chain_check_kernel must
-      // then report the launch as incomplete)
       int drop = 0;
+#ifdef RT_DIAG
+      // (fault injection, diagnostic build only: drop the item unrun and uncounted -- chain_check_kernel
+      // must then report the launch as incomplete)
       if (V.mig_drop && l0) drop = atomicAdd(&V.mig[kMigDropped], 1u) < V.mig_drop;
+#endif
       if (!__builtin_amdgcn_readfirstlane(drop)) {
         __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
-        render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r, V.rq != nullptr);
+        render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
         __builtin_amdgcn_s_setprio(0);
-        if (l0 && !seg_dynamic(V, r.pix, r.seg)) mig_item_done(V, total_own);  // (a cut is no item of the launch)
+        if (l0) mig_item_done(V, total_own);
       }
       if (l0) atomicAdd(box + kMigCredits, 1u);
       idle_since = wall_clock64();
       continue;
     }
     if (__builtin_amdgcn_readfirstlane(fin)) break;
-    // Nothing migrated to run: a re-cut request?  The helper first takes back its credit (so no lane
-    // queues an item to it while it runs a segment), and gives it again afterwards.
-    if (V.rq) {
-      int req = -1;
-      if (l0 && ld_rel(&V.mig[kMigRqPop]) < ld_rel(&V.mig[kMigRqPush])) {
-        uint32_t c = ld_rel(box + kMigCredits);
-        bool mine = false;
-        while ((int32_t)c > 0 && !mine) {
-          const uint32_t prev = atomicCAS(box + kMigCredits, c, c - 1u);
-          mine = prev == c;
-          c = prev;
-        }
-        if (mine) {
-          req = recut_pop(V);
-          if (req < 0) atomicAdd(box + kMigCredits, 1u);
-        }
-      }
-      req = __builtin_amdgcn_readfirstlane(req);
-      if (req >= 0) {
-        uint32_t t = 0u, pix = 0u;
-        if (l0) {
-          const RecutReq r = V.rq[(uint32_t)req];
-          t = recut_publish(V, r);
-          pix = r.pix;
-        }
-        t = wv_first(t);
-        if (t) {
-          __builtin_amdgcn_s_setprio(2);
-          render_item_coop<kMode>(V, items9, (int64_t)wv_first(pix), t, out, nullptr, true);
-          __builtin_amdgcn_s_setprio(0);
-        }
-        if (l0) atomicAdd(box + kMigCredits, 1u);
-        idle_since = wall_clock64();
-        continue;
-      }
-    }
     // A helper idle for mig_wait leaves -- but only by taking back a credit that no push has claimed.
     // A claimed credit stands for an item that is (being) queued in this mailbox, which then still
     // has a helper to run it; so no item is ever queued to a mailbox whose helpers have all left.
@@ -1204,11 +948,7 @@ __device__ __attribute__((noinline)) void coop_items(const Book1View &V, const f
   }
 }
 
-// kIdle: a chain-launch lane with no work item left; a lane of its wave may hand it a cut (below)
-enum : int { kTrav = 0, kWait = 1, kExit = 2, kIdle = 3 };
-// LDS behind the scene items (chain launches): per lane a handed-over cut {pixel, segment} (segment 0:
-// none), per wave the mask of idle lanes not yet handed one
-constexpr size_t kHandoffBytes = kBlock * sizeof(uint2) + kWaves * sizeof(unsigned long long);
+enum : int { kTrav = 0, kWait = 1, kExit = 2 };
 // traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
 // 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
 // schedule never changes a lane)
@@ -1216,9 +956,7 @@ constexpr int kSteps = 16;
 
 // The lane kernel.  kMode: 0 frame (whole pixels), 1 cost pre-pass (also counts draws per item),
 // 2 chain render (items of ch_items, or the continuation items of ch_cont).
-// kRecut: the run-time re-cut paths (RT_RECUT=1) compiled in -- a separate instantiation, so that
-// their registers do not enter the default chain kernel's loop (they cost it 8 SGPR reloads a step).
-template <bool kLds, int kMode = 0, bool kRecut = false>
+template <bool kLds, int kMode = 0>
 __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, char *lds) {
   const int tid = threadIdx.x;
   const bool cont = kMode == 2 && V.ch_cont != nullptr;
@@ -1258,19 +996,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
   uint64_t mig_next = 0;
-  bool dyn = false;        // this lane runs a cut (a dynamic segment), not one of the launch's items
-  bool cut_ready = false;  // a cut was handed to this idle lane: its next item
-  // intra-wave cuts (chain launches): handoff slots and idle masks in LDS behind the scene items
-  uint2 *handoff = nullptr;
-  unsigned long long *idle_lds = nullptr;
-  const bool cuts = kRecut && kMode == 2 && V.recut_lanes != 0 && !cont;
-  if (kMode == 2 && kRecut) {  // (the default instantiation has no handoff region: occupancy 5 needs the LDS)
-    char *hb = lds + (kLds ? (size_t)V.n_items9_alloc * 2 * sizeof(float4) : 0);
-    handoff = (uint2 *)hb;
-    idle_lds = (unsigned long long *)(hb + kBlock * sizeof(uint2));
-    handoff[tid] = make_uint2(0u, 0u);
-  }
-  const int wave_in_block = tid >> 6;
   bool have_result = false;  // false: this lane first needs a work item
   uint32_t px_steps = 0;
   int32_t pix = 0;  // (< 2^31: host-checked)
@@ -1299,21 +1024,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
                                          : total - work_offset;
 
   for (;;) {
-    if (cuts && mode == kIdle) {  // a cut handed to this idle lane by a lane of its wave?
-      const uint2 h = handoff[tid];
-      if (h.y) {
-        handoff[tid].y = 0u;
-        pix = (int32_t)h.x;
-        seg = h.y;
-        cut_ready = true;
-        have_result = false;
-        mode = kWait;
-      }
-    }
     const uint64_t trav = __ballot(mode == kTrav);
     const uint64_t wait = __ballot(mode == kWait);
     if ((trav | wait) == 0) break;
-    const uint64_t idle = cuts ? __ballot(mode == kIdle) : 0ull;
     // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
@@ -1342,11 +1055,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #pragma unroll
           for (int u = 0; u < kSteps; u++)
             if (mode == kTrav) {
-              if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
-              if (trav_step_v9(items9, na, n9, L, tmin)) mode = kWait;
+              const uint32_t at = L.cur;
+              if (trav_step_v9(items9, na, n9, L, tmin, V.leaf_min)) mode = kWait;
+              if (kMode == 1) px_steps += L.cur != at;  // work-item cost (the LPT pre-pass): items visited
             }
         }
-        if (cuts) break;  // (the loop top hands cuts to idle lanes between passes)
         const uint64_t t2 = __ballot(mode == kTrav), w2 = __ballot(mode == kWait);
         const int batch2 = min(V.shade_batch, (3 * (int)__popcll(t2 | w2) + 3) / 4);
         if (t2 == 0ull || (int)__popcll(w2) >= batch2) break;
@@ -1364,7 +1077,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       continue;
     }
     if (mode != kWait) continue;
-    if (cuts && idle && lane == __builtin_ctzll(wait)) idle_lds[wave_in_block] = idle;  // (this pass's idle lanes)
     // migration: the work items are gone (a lane of this wave found none) and few lanes are left
     // and enough of the GPU idles (more than mig_idle waves have become helpers): before that,
     // whole-wave traces would take issue slots from lanes that still make full use of them.  The
@@ -1434,21 +1146,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       }
     }
     while (need_pixel || need_sample) {
-      if (need_pixel && kMode == 2 && cut_ready) {  // a cut a lane of this wave handed over: run it
-        cut_ready = false;
-        dyn = true;
-        acc = mk(0.0f, 0.0f, 0.0f);
-        s = 0;
-        tc = kNoTarget;
-        {
-          const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
-          g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
-        }
-        chain_start(V, (uint32_t)pix, seg, g, tc, st);
-        need_pixel = false;
-        px_steps = 0;
-        if (V.px_time) chain_time(V, pix, seg, 0);
-      }
       if (need_pixel) {  // work stealing among the lanes that need an item right now
         const uint64_t want = __ballot(true);
         const int first = __builtin_ctzll(want);
@@ -1456,35 +1153,20 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (lane == first) base = atomicAdd(V.work_counter, (int)__popcll(want));
         base = __shfl(base, first);
         const int64_t item = (int64_t)base + __popcll(want & ((1ull << lane) - 1));
-        // no item left: a whole-wave helper's queued cut, if any (RecutReq); else this lane is done --
-        // idle, where a lane of its wave may still hand it a cut of its own chain
-        uint32_t cut = 0u, cut_pix = 0u;
-        if (kRecut && kMode == 2 && item >= total_own && V.rq && !cuts) {
-          const int req = recut_pop(V);
-          if (req >= 0) {
-            const RecutReq r = V.rq[(uint32_t)req];
-            cut = recut_publish(V, r);
-            cut_pix = r.pix;
-          }
-        }
-        if (item >= total_own && cut == 0u) {
-          mode = cuts ? kIdle : kExit;
+        if (item >= total_own) {  // no item left: this lane is done
+          mode = kExit;
           break;
         }
         acc = mk(0.0f, 0.0f, 0.0f);
         s = 0;
         seg = kItemUnsplit;
         tc = kNoTarget;
-        dyn = cut != 0u;
         if (kMode == 2 && cont) {  // the true chain on from an exact position (chain_fold_kernel)
           const ChainCont c = V.ch_cont[item];
           pix = (int32_t)c.pix;
           s = (int)c.s;
           acc = mk(c.acc[0], c.acc[1], c.acc[2]);
           st = c.o;  // (applied below, after the seed)
-        } else if (kMode == 2 && dyn) {
-          pix = (int32_t)cut_pix;
-          seg = cut;
         } else if (kMode == 2) {
           const uint2 it = V.ch_items[item + work_offset];
           pix = (int32_t)it.x;
@@ -1507,35 +1189,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }
       if (kMode == 2 && chain_boundary(V, pix, seg, g.n, (uint32_t)s, acc, tc, st, out, true)) {
-        if (kMode == kMigMode && V.mig_live > 0 && !dyn) mig_item_done(V, total_own);
+        if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
         need_pixel = true;  // this item is finished
         continue;
-      }
-      // the launch's tail: this wave has idle lanes -- a long chain hands one of them a cut of itself
-      if (cuts && idle && (s & 3) == 0 && idle_lds[wave_in_block] != 0ull) {
-        RecutReq r;
-        if (recut_plan(V, (uint32_t)pix, seg, g.n, (uint32_t)s, tc, r)) {
-          unsigned long long m = idle_lds[wave_in_block], bit = 0ull;
-          while (m) {  // claim an idle lane (another lane of this wave may claim at the same time)
-            const unsigned long long b = m & (~m + 1ull);
-            const unsigned long long old = atomicAnd(&idle_lds[wave_in_block], ~b);
-            if (old & b) {
-              bit = b;
-              break;
-            }
-            m = old & ~b;
-          }
-          if (bit) {
-            const uint32_t t = recut_publish(V, r);
-            if (t) {
-              handoff[(wave_in_block << 6) + __builtin_ctzll(bit)] = make_uint2((uint32_t)pix, t);
-              tc |= kWatch;
-            } else {  // (no cut: the pixel's dynamic slots or the records are used up -- do not ask again)
-              atomicOr(&idle_lds[wave_in_block], bit);
-              tc |= kNoAsk;
-            }
-          }
-        }
       }
       if (mig_try && !need_pixel && mig_push(V, (uint32_t)glane % kMigBoxes, pix, seg, (uint32_t)s, acc, g, tc, st)) {
         mode = kExit;  // handed over at this sample boundary
@@ -1575,7 +1231,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
       }
     }
-    if (mode == kExit || mode == kIdle) continue;  // (no item: no new ray)
+    if (mode == kExit) continue;  // (no item: no new ray)
     // set up the traversal of the new ray
     L.ix = 1.0f / L.dx, L.iy = 1.0f / L.dy, L.iz = 1.0f / L.dz;
     L.a = dot(mk(L.dx, L.dy, L.dz), mk(L.dx, L.dy, L.dz));
@@ -1631,16 +1287,16 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     acc = mk(a0.x, a0.y, a0.z);
     total = end_n(w);
     t = end_t(w), c = end_c(w);
-    o = c == 0 ? seg_start(V, P, t) : V.ch_end[rec_index(V, P, t, c - 1u)];
+    o = c == 0 ? seg_start(P, t) : V.ch_end[rec_index(P, t, c - 1u)];
   }
   while (linked && total < spp) {
-    if (t == 0 || t >= P.K + kDynMax) break;  // (never: links point forward)
+    if (t == 0 || t >= P.K) break;  // (never: links point forward)
     w = V.ch_seg[P.end0 + t];
     const uint32_t n = end_n(w);
     const uint32_t m = n > c ? min(n - c, spp - total) : 0u;
     for (uint32_t b = 0; b < m; b += 64) {
       float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (b + (uint32_t)lane < m) r = V.ch_col[rec_index(V, P, t, c + b + (uint32_t)lane)];
+      if (b + (uint32_t)lane < m) r = V.ch_col[rec_index(P, t, c + b + (uint32_t)lane)];
       const uint32_t cnt = min(64u, m - b);
       for (uint32_t q = 0; q < cnt; q++)
         acc = add(acc, mk(lane_bcast(r.x, (int)q), lane_bcast(r.y, (int)q), lane_bcast(r.z, (int)q)));

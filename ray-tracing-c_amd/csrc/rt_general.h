@@ -28,15 +28,16 @@ struct GeneralView {
                              // flat - 1 box entries in the same step (RT_GEN_FLAT, >= 1)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
   int32_t perlin_lds;        // kAllLds: byte offset of perlins[0]'s LDS copy (PerlinLds) behind the preorder; -1: none
-  float4 *xrec;              // explicit albedos of path records: kMaxDepth per thread of the grid, thread-contiguous
-  float *xw;                 // pdf weights of path records: kMaxDepth per thread of the grid, thread-contiguous
+  float4 *xrec;              // explicit albedos of path records beyond the register stack (XStack): kMaxDepth
+                             // per thread of the grid, thread-contiguous
+  float *xw;                 // pdf weights beyond the register stack (RegStack): kMaxDepth per thread
   int32_t code_bits;         // 4 (scenes of <= 13 textures) or 8: width of a path record's albedo code
 };
 
 // Path records as runs of codes in one u64 register pair (PathRuns).  A record's code is its albedo
 // in b bits (b = code_bits) -- 1..2^b - 3 = the colour of solid texture code - 1, 2^b - 2 = (1, 1, 1),
-// 2^b - 1 = explicit: the albedo is in the thread's xrec slot (image / noise textures, textures past
-// the code range) -- and bit b: weighted, the pdf weight is in the thread's xw slot.  Consecutive
+// 2^b - 1 = explicit: the albedo is on the lane's explicit-albedo stack (XStack: image / noise textures,
+// textures past the code range) -- and bit b: weighted, the pdf weight is on its weight stack.  Consecutive
 // bounces of one code (a random walk in a medium: scene 7's subsurface sphere runs every such path
 // to max_depth) are one run of (code, length - 1: 6 bits); bits 60..63 count the runs, 15 = full:
 // the bounces past the runs are explicit and weighted (weight 1 when the bounce had none:
@@ -76,6 +77,62 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
   R.w |= 15ull << 60;
   return false;
 }
+
+// The records' explicit albedos and pdf weights as two LIFO stacks whose newest entries sit in
+// registers (the fold visits records newest first, i.e. in reverse push order): a push into a full
+// register part moves its oldest entry to the thread's global slots, a pop refills the register part
+// from there.  Scene 7 averages 4.37 records per sample, 3.9 of them weighted and 0.65 explicit
+// (DESIGN.md §4.3); with 8 weights and 2 albedos in registers nearly no path touches memory, where
+// every record store used to leave L2 for HBM at >= 32 B.  Only static register indices (unrolled
+// shifts): a dynamically indexed private array would live in scratch.
+template <int kN>
+struct RegStack {
+  float v[kN];
+  int n;  // entries pushed and not popped (the newest min(n, kN) in v, newest first)
+};
+template <int kN>
+RT_D void rs_clear(RegStack<kN> &S) { S.n = 0; }
+template <int kN>
+RT_D void rs_push(RegStack<kN> &S, float x, float *spill) {
+  if (S.n >= kN) spill[S.n - kN] = S.v[kN - 1];
+#pragma unroll
+  for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
+  S.v[0] = x;
+  S.n++;
+}
+template <int kN>
+RT_D float rs_pop(RegStack<kN> &S, const float *spill) {
+  const float x = S.v[0];
+#pragma unroll
+  for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
+  S.n--;
+  if (S.n >= kN) S.v[kN - 1] = spill[S.n - kN];
+  return x;
+}
+struct XStack {  // explicit albedos: kXReg in registers
+  static constexpr int kN = 2;
+  f3 v[kN];
+  int n;
+};
+RT_D void xs_push(XStack &S, f3 x, float4 *spill) {
+  if (S.n >= XStack::kN) spill[S.n - XStack::kN] = make_float4(S.v[XStack::kN - 1].x, S.v[XStack::kN - 1].y, S.v[XStack::kN - 1].z, 0.0f);
+#pragma unroll
+  for (int k = XStack::kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
+  S.v[0] = x;
+  S.n++;
+}
+RT_D f3 xs_pop(XStack &S, const float4 *spill) {
+  const f3 x = S.v[0];
+#pragma unroll
+  for (int k = 0; k < XStack::kN - 1; k++) S.v[k] = S.v[k + 1];
+  S.n--;
+  if (S.n >= XStack::kN) {
+    const float4 e = spill[S.n - XStack::kN];
+    S.v[XStack::kN - 1] = mk(e.x, e.y, e.z);
+  }
+  return x;
+}
+constexpr int kWReg = 8;  // pdf weights in registers
 
 // -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
 enum {
@@ -436,15 +493,20 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   // emission is always +0 (only SurfaceNormal and DiffuseLight emit, and neither scatters:
   // src/material.c:103-142), so the record is (albedo, pdf weight) and the fold adds +0 as the
   // reference's vec3_add(emission_color, scatter_color) does.  Records: albedo codes (kCode*) in
-  // registers, explicit ones in the thread's xrec slots (thread-contiguous: a lane's records share
+  // registers, explicit ones on register stacks spilling to the thread's slots (a lane's records share
   // cache lines, where private arrays interleave every dword across the wave's lanes).
   PathRuns runs = runs_init(V.code_bits);
   const uint32_t code_explicit = (1u << runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << runs.cb;
-  // (every store leaves L2 for the fabric, at least a 32-B sector each: weights are stored in pairs,
-  // one 8-B store per two bounces, the even bounce's weight waiting in wpend)
+  // (explicit albedos and weights in register stacks, RegStack / XStack; their overflow in the thread's
+  // kMaxDepth global slots)
   const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
-  float wpend = 0.0f;
-  bool wprev = false;  // the previous (even) bounce was weighted: its weight is in wpend
+  RegStack<kWReg> wst;
+  XStack xst;
+#pragma unroll
+  for (int k = 0; k < kWReg; k++) wst.v[k] = 1.0f;
+#pragma unroll
+  for (int k = 0; k < XStack::kN; k++) xst.v[k] = mk(0.0f, 0.0f, 0.0f);
+  wst.n = 0, xst.n = 0;
   int n = 0, depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
   uint32_t rays = 0;
@@ -615,6 +677,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       depth = S.cam.max_depth;
       n = 0;
       runs.w = 0;
+      wst.n = 0, xst.n = 0;
       need_sample = false;
     }
     GS_ADD(kGsCycCamera, GS_NOW() - gs_c);
@@ -699,14 +762,8 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             }
           }
           if (!runs_push(runs, code)) code = code_explicit | code_weighted;
-          if ((code & code_explicit) == code_explicit) V.xrec[rec0 + n] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
-          const bool wt = (code & code_weighted) != 0;
-          if ((n & 1) == 0) {
-            wpend = w;
-            wprev = wt;
-          } else if (wt || wprev) {
-            *(float2 *)(V.xw + rec0 + n - 1) = make_float2(wpend, w);
-          }
+          if ((code & code_explicit) == code_explicit) xs_push(xst, albedo, V.xrec + rec0);
+          if (code & code_weighted) rs_push(wst, w, V.xw + rec0);
           GS_ADD(kGsRecords, 1);  // (per lane: summed over every lane at the end)
           GS_ADD(kGsExplicit, (code & code_explicit) == code_explicit);
           GS_ADD(kGsWeighted, (code & code_weighted) != 0);
@@ -747,12 +804,9 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           }
           left--;
         }
-        if ((code & code_explicit) == code_explicit) {
-          const float4 e = V.xrec[rec0 + k];
-          a = mk(e.x, e.y, e.z);
-        }
+        if ((code & code_explicit) == code_explicit) a = xs_pop(xst, V.xrec + rec0);
         f3 x = mul(a, c);
-        if (code & code_weighted) x = scale(x, (k & 1) == 0 && k == n - 1 ? wpend : V.xw[rec0 + k]);
+        if (code & code_weighted) x = scale(x, rs_pop(wst, V.xw + rec0));
         c = add(mk(0.0f, 0.0f, 0.0f), x);
       }
     }

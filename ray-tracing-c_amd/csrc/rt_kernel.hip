@@ -87,17 +87,16 @@ __global__ __launch_bounds__(kBlock) void rt_render_deep_kernel(DScene S, int ro
 // chain kernel, its cost pre-pass and the lane kernel run at 5 waves per SIMD (96 VGPRs; the chain
 // kernel spills 15, none in the traversal loop: 270 ms vs 282 ms at 4 waves; with the
 // SLP vectorizer's packed f32 ops it needed 128 and spilled 65 at 5); launches with few pixels per lane
-// (N >= 2 shares) use the 3-wave instantiation (launch_chain); the re-cut variant runs at 4 (its
-// intra-wave handoff region in LDS does not fit 5 workgroups beside the scene).
+// (N >= 2 shares) use the 3-wave instantiation (launch_chain).
 template <bool kLds>
 __global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 0>(V, out, lds);
 }
-template <bool kLds, bool kRecut = false, int kOcc = 5>
-__global__ __launch_bounds__(b1::kBlock, kRecut ? 4 : kOcc) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_chain_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  b1::render_batched<kLds, 2, kRecut>(V, out, lds);
+  b1::render_batched<kLds, 2>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
 template <bool kLds>
@@ -334,7 +333,7 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
                                                          uint32_t *cnt, ChainModel m, b1::ChainPx *px,
-                                                         uint64_t *seg, b1::SegDyn *sd, uint32_t *kk, uint32_t *split) {
+                                                         uint64_t *seg, uint32_t *kk, uint32_t *split) {
   __shared__ uint32_t h[256];
   __shared__ unsigned long long wwork;
   for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
@@ -376,8 +375,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       const uint32_t need = (uint32_t)(K - 2) * cap + cap_last;
       const unsigned long long r0 = atomicAdd((unsigned long long *)&cnt[kCnRec], (unsigned long long)need);
       const bool fits = r0 + need <= (unsigned long long)m.rec_cap;
-      // end words: K planned segments + kDynMax dynamic ones (run-time re-cut)
-      const uint32_t n_end = (uint32_t)K + b1::kDynMax;
+      const uint32_t n_end = (uint32_t)K;  // end words
       const uint32_t e0 = fits ? atomicAdd(&cnt[kCnSeg], n_end) : 0xffffffffu;
       if (!fits || (uint64_t)e0 + n_end > (uint64_t)m.seg_cap) {
         K = 1;  // out of record / end-word space: this pixel stays whole (the reservation is left unused)
@@ -390,9 +388,9 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
         P.end0 = e0;
         P.check = (uint32_t)(3 * (m.spp / K) / 4);
         P.cap_last = cap_last;
-        P.kd = 0u;
+        P.pad = 0u;
         px[p] = P;
-        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull, sd[e0 + k].next = 0u;  // (planned successors)
+        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull;
         split[atomicAdd(&cnt[kCnSplit], 1u)] = (uint32_t)p;
       }
     }
@@ -481,11 +479,9 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
   for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = make_uint2((uint32_t)(val[i] >> 32), (uint32_t)val[i]);
 }
 
-// ch_end = kRecFill for the planned records and a reserve behind them, from which run-time cuts
-// (rt_book1.h: recut_publish) allocate their record lists; cnt[kCnFilled] = the end of the filled range.
-constexpr unsigned long long kRecutReserve = 16u << 20;  // records (64 MB of end words)
+// ch_end = kRecFill for the planned records; cnt[kCnFilled] = the end of the filled range.
 __global__ void chain_fill_kernel(uint32_t *cnt, uint32_t *ch_end, uint32_t cap) {
-  const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec] + kRecutReserve;
+  const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kCnFilled] = n;
   const uint32_t n4 = n / 4;
@@ -516,7 +512,7 @@ __global__ void chain_check_kernel(const uint32_t *mig, const uint32_t *n_items,
 }
 
 // ------------------------------------------------------------------------------ configuration
-static bool env_flag(const char *name, bool dflt) {
+[[maybe_unused]] static bool env_flag(const char *name, bool dflt) {  // (the diagnostic build's switches)
   const char *e = getenv(name);
   if (!e || !*e) return dflt;
   return !(e[0] == '0' || e[0] == 'n' || e[0] == 'N' || e[0] == 'f' || e[0] == 'F');
@@ -532,11 +528,12 @@ static float env_float(const char *name, float dflt) {
 
 enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 
-// Every knob, read once per scene upload (INTEGRATION.md lists them).
+// Every knob, read once per scene upload (INTEGRATION.md lists them): the product library reads the
+// planner / scheduling parameters only; the diagnostic build (-DRT_DIAG) also the A/B switches.
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
   bool lpt = true, bf = true, px_time = false, debug = false;
-  int lpt_spp = 16, shade_batch = 48;
+  int lpt_spp = 16, shade_batch = 48, leaf_min = 1;
   int mode = kModeAuto;
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
@@ -552,33 +549,33 @@ struct Config {
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
-  bool recut = false;      // run-time re-cuts in a launch's tail (rt_book1.h: RecutReq; measured slower at N = 8: opt-in)
-  int recut_min = 32;      //   of chains with at least this many samples left
-  float recut_frac = 0.5f; //   the chain keeps this share of its remaining draws
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
-  int chain_occ = 0;          // chain kernel waves per SIMD: 3, 4, 5, or 0 = by pixels per lane (below)
+  int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
                               //   same box, N = 1 / 2 / 4 / 8: 3 waves 268 / 168 / 100 / 68.5 ms, 4 waves
                               //   274-277 / 172-180 / 102-104 / 69-70, 5 waves 265-267 / 172-177 / 105 / 70-73)
   static Config from_env() {
     Config c;
+    // the documented planner / scheduling parameters
+    c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
+    if (c.lpt_spp < 1) c.lpt_spp = 1;
+    c.chain_beta = env_float("RT_CHAIN_BETA", c.chain_beta);
+    c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ);
+    c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
+    c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
-    c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
     c.mig_wait_us = env_int("RT_MIG_WAIT_US", c.mig_wait_us);
     if (c.mig_wait_us < 0) c.mig_wait_us = 0;
+#ifdef RT_DIAG
+    // the diagnostic build only (librtc_amd_diag.so, -DRT_DIAG): path selection for tests, A/B
+    // switches of the measured alternatives, timelines, fault injection
     c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
-    c.recut = env_flag("RT_RECUT", c.recut);
-    c.recut_min = env_int("RT_RECUT_MIN", c.recut_min);
-    if (c.recut_min < 4) c.recut_min = 4;
-    c.recut_frac = env_float("RT_RECUT_FRAC", c.recut_frac);
-    c.recut_frac = c.recut_frac < 0.05f ? 0.05f : (c.recut_frac > 0.95f ? 0.95f : c.recut_frac);
     if (c.mig_drop < 0) c.mig_drop = 0;
-    c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
-    c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
+    c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
     c.general = env_flag("RT_GENERAL", true);
@@ -587,15 +584,14 @@ struct Config {
     c.bf = env_flag("RT_BF", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
-    c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
-    if (c.lpt_spp < 1) c.lpt_spp = 1;
-    c.shade_batch = env_int("RT_SHADE_BATCH", 48);
+    c.leaf_min = env_int("RT_LEAF_MIN", c.leaf_min);
+    c.leaf_min = c.leaf_min < 1 ? 1 : (c.leaf_min > 64 ? 64 : c.leaf_min);
+    c.shade_batch = env_int("RT_SHADE_BATCH", c.shade_batch);
     c.shade_batch = c.shade_batch < 1 ? 1 : (c.shade_batch > 64 ? 64 : c.shade_batch);  // >= 1: progress
     if (const char *m = getenv("RT_MODE")) {
       if (!strcmp(m, "lane")) c.mode = kModeLane;
       else if (!strcmp(m, "chain")) c.mode = kModeChain;
     }
-    c.chain_beta = env_float("RT_CHAIN_BETA", c.chain_beta);
     c.chain_margin = env_float("RT_CHAIN_MARGIN", c.chain_margin);
     if (c.chain_margin < 1.0f) c.chain_margin = 1.0f;
     c.chain_kmax = env_int("RT_CHAIN_KMAX", c.chain_kmax);
@@ -609,13 +605,12 @@ struct Config {
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
-    c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ);
     c.chain_occ_px = env_float("RT_CHAIN_OCC_PX", c.chain_occ_px);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
-    c.gen_batch = env_int("RT_GEN_BATCH", 56);
+    c.gen_batch = env_int("RT_GEN_BATCH", c.gen_batch);
     c.gen_batch = c.gen_batch < 0 ? 0 : (c.gen_batch > 64 ? 64 : c.gen_batch);
-    c.gen_lds = env_int("RT_GEN_LDS", 1024);
+    c.gen_lds = env_int("RT_GEN_LDS", c.gen_lds);
     c.gen_big = env_flag("RT_GEN_BIG", true);
     c.gen_perlin = env_flag("RT_GEN_PERLIN_LDS", true);
     c.gen_steps = env_int("RT_GEN_STEPS", c.gen_steps);
@@ -623,6 +618,7 @@ struct Config {
     c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
     c.gen_flat = env_int("RT_GEN_FLAT", c.gen_flat);
     if (c.gen_flat < 1) c.gen_flat = 1;
+#endif
     return c;
   }
 };
@@ -646,7 +642,7 @@ struct rt_device_scene {
   void *b1_arena = nullptr;
   size_t b1_lds_bytes = 0;
   int b1_grid = 0, chain_grid = 0;  // chain_grid: the current chain launch's (one of the two below)
-  int chain_grid5 = 0, chain_grid4 = 0, chain_grid3 = 0, chain_occ = 5;  // chain kernel grids at 5 / 4 / 3 waves per SIMD
+  int chain_grid5 = 0, chain_grid3 = 0, chain_occ = 5;  // chain kernel grids at 5 / 3 waves per SIMD
   uint32_t *lpt_cost = nullptr;  // pre-pass steps per work item (W*H)
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
@@ -666,9 +662,6 @@ struct rt_device_scene {
   float4 *ch_acc0 = nullptr;
   b1::ChainCont *ch_cont = nullptr;
   uint32_t ch_seg_cap = 0;
-  b1::SegDyn *ch_sd = nullptr;      // per segment slot: dynamic segments, successor words (run-time re-cut)
-  b1::RecutReq *rq = nullptr;       // re-cut request queue
-  uint32_t rq_cap = 0;
   void *ch_rec_arena = nullptr;
   size_t ch_rec_cap = 0;  // records
   // general path (rt_general.h) for scenes outside the Book-1 path
@@ -898,31 +891,21 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->b1_lds_bytes = align_up(lds ? items_bytes : 0, 16);
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->device));
-  int per_cu = 0, per_cu_chain = 0, per_cu_chain4 = 0, per_cu_chain3 = 0;
+  int per_cu = 0, per_cu_chain = 0, per_cu_chain3 = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, lds ? (const void *)rt_book1_kernel<true> : (const void *)rt_book1_kernel<false>, b1::kBlock,
       d->b1_lds_bytes));
-  if (cfg.recut)  // (the re-cut instantiation: occupancy 4, the intra-wave cut handoff behind the scene)
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true, true> : (const void *)rt_book1_chain_kernel<false, true>,
-        b1::kBlock, d->b1_lds_bytes + b1::kHandoffBytes));
-  else
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
-        b1::kBlock, d->b1_lds_bytes));
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_chain4, lds ? (const void *)rt_book1_chain_kernel<true, false, 4> : (const void *)rt_book1_chain_kernel<false, false, 4>,
+      &per_cu_chain, lds ? (const void *)rt_book1_chain_kernel<true> : (const void *)rt_book1_chain_kernel<false>,
       b1::kBlock, d->b1_lds_bytes));
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_chain3, lds ? (const void *)rt_book1_chain_kernel<true, false, 3> : (const void *)rt_book1_chain_kernel<false, false, 3>,
+      &per_cu_chain3, lds ? (const void *)rt_book1_chain_kernel<true, 3> : (const void *)rt_book1_chain_kernel<false, 3>,
       b1::kBlock, d->b1_lds_bytes));
-  if (cfg.recut) per_cu_chain4 = per_cu_chain3 = per_cu_chain;  // (one instantiation, occupancy 4)
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid5 = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
-  d->chain_grid4 = prop.multiProcessorCount * (per_cu_chain4 < 1 ? 1 : per_cu_chain4);
   d->chain_grid3 = prop.multiProcessorCount * (per_cu_chain3 < 1 ? 1 : per_cu_chain3);
   d->chain_grid = d->chain_grid5;
-  const int chain_max = d->chain_grid5 > d->chain_grid4 ? d->chain_grid5 : d->chain_grid4;
+  const int chain_max = d->chain_grid5 > d->chain_grid3 ? d->chain_grid5 : d->chain_grid3;
   const int spill_grid = d->b1_grid > chain_max ? d->b1_grid : chain_max;
   const int spill_lanes = spill_grid * b1::kBlock;
   // path record chunks beyond the two in registers (Record): ceil(max_depth / 4) - 2 per lane
@@ -969,6 +952,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.spill = (uint64_t *)(b + off[3]);
   V.spill_lanes = spill_lanes;
   V.shade_batch = cfg.shade_batch;
+  V.leaf_min = cfg.leaf_min;
   V.n_bf_leaves = H.n_bf;
   d->lpt_cost = (uint32_t *)(b + off[4]);
   d->lpt_order = (int32_t *)(b + off[5]);
@@ -985,15 +969,13 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   // chain scratch for the whole frame (a launch covers at most every pixel)
   {
     const int kmax = cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave;
-    const size_t nitem = npix * (size_t)kmax, nseg = npix * (size_t)(kmax + b1::kDynMax);
+    const size_t nitem = npix * (size_t)kmax, nseg = npix * (size_t)kmax;
     d->ch_seg_cap = nseg < 0xffffffffu ? (uint32_t)nseg : 0xffffffffu;
-    d->rq_cap = (uint32_t)(2 * npix + 4096 < 0x7fffffffu ? 2 * npix + 4096 : 0x7fffffffu);
-    const size_t cs[11] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
-                           npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
-                           nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont),
-                           nseg * sizeof(b1::SegDyn), (size_t)d->rq_cap * sizeof(b1::RecutReq)};
-    size_t co[11], ct = 0;
-    for (int k = 0; k < 11; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
+    const size_t cs[9] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
+                          npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
+                          nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont)};
+    size_t co[9], ct = 0;
+    for (int k = 0; k < 9; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
     HIP_OK(hipMalloc(&d->ch_arena, ct));
     char *c = (char *)d->ch_arena;
     d->ch_cnt = (uint32_t *)(c + co[0]);
@@ -1005,8 +987,6 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_wave_key = (uint64_t *)(c + co[6]);
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
-    d->ch_sd = (b1::SegDyn *)(c + co[9]);
-    d->rq = (b1::RecutReq *)(c + co[10]);
     if (cfg.px_time) {
       HIP_OK(hipMalloc(&d->seg_time, nseg * 2 * sizeof(uint32_t)));
       V.seg_time = d->seg_time;
@@ -1216,20 +1196,10 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
 
 static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V, uint8_t *d_out, hipStream_t st) {
   const dim3 gc((unsigned)d->chain_grid), blk(b1::kBlock);
-  const size_t lds = d->b1_lds_bytes, bytes = lds + b1::kHandoffBytes;  // (+ the intra-wave cut handoff)
-  if (d->cfg.recut) {  // RT_RECUT=1: the instantiation with the re-cut paths
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, true>), gc, blk, bytes, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, true>), gc, blk, bytes, st, V, d_out);
-    return;
-  }
+  const size_t lds = d->b1_lds_bytes;
   if (d->chain_occ == 3) {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, false, 3>), gc, blk, lds, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, false, 3>), gc, blk, 0, st, V, d_out);
-    return;
-  }
-  if (d->chain_occ == 4) {
-    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, false, 4>), gc, blk, lds, st, V, d_out);
-    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, false, 4>), gc, blk, 0, st, V, d_out);
+    if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true, 3>), gc, blk, lds, st, V, d_out);
+    else hipLaunchKernelGGL((rt_book1_chain_kernel<false, 3>), gc, blk, 0, st, V, d_out);
     return;
   }
   if (lds) hipLaunchKernelGGL((rt_book1_chain_kernel<true>), gc, blk, lds, st, V, d_out);
@@ -1258,19 +1228,21 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp) {
 
 // Chain launch (rt_book1.h: ChainPx): cost pre-pass, device-side plan, the chains (lanes + whole
 // waves), the fold, and a continuation launch for whatever the fold could not finish.  No host sync.
+// The chain kernel's waves per SIMD for a launch of npix pixels (RT_CHAIN_OCC, else by pixels per lane).
+static int chain_occupancy(const rt_device_scene *d, int64_t npix) {
+  const int occ = d->cfg.chain_occ;
+  if (occ == 3 || occ == 5) return occ;
+  return (double)npix >= d->cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 3;
+}
+
 static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
   const Config &cfg = d->cfg;
   if (chain_records(d, (size_t)npix, V.S.cam.spp) != 0) return -1;
   // waves per SIMD: 5 hide more latency (headline frame 266 vs 275 ms at 4), 3 run each lane chain
   // faster with no spills at all (168 VGPRs) -- what a launch with few pixels per lane needs (its time
   // is its longest chains)
-  {
-    int occ = cfg.chain_occ;
-    if (cfg.recut) occ = 4;
-    else if (occ < 3 || occ > 5) occ = (double)npix >= cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 3;
-    d->chain_occ = occ;
-    d->chain_grid = occ == 5 ? d->chain_grid5 : occ == 4 ? d->chain_grid4 : d->chain_grid3;
-  }
+  d->chain_occ = chain_occupancy(d, npix);
+  d->chain_grid = d->chain_occ == 5 ? d->chain_grid5 : d->chain_grid3;
   launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
@@ -1306,7 +1278,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   uint32_t *end = (uint32_t *)(col + d->ch_rec_cap);
   hipLaunchKernelGGL(chain_params_kernel, dim3(1), dim3(64), 0, st, sums, d->ch_cnt, m);
   hipLaunchKernelGGL(chain_plan_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, d->draw_out, n, d->ch_cnt, m, d->ch_px,
-                     d->ch_seg, d->ch_sd, d->ch_k, d->ch_split);
+                     d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
                      d->ch_wave_key);
@@ -1339,18 +1311,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
-  V.ch_sd = d->ch_sd;
-  V.rec_count = (unsigned long long *)(d->ch_cnt + kCnRec);
-  V.rec_filled = d->ch_cnt + kCnFilled;
-  V.recut_lanes = cfg.recut ? 1 : 0;  // intra-wave cuts: a lane hands an idle lane of its wave a cut
-  V.recut_min = (uint32_t)cfg.recut_min;
-  V.recut_frac = cfg.recut_frac;
-  V.recut_slack = (uint32_t)cfg.chain_slack;
-  V.recut_stats = d->status + 4;
-  if (cfg.recut && V.mig_live > 0 && d->b1_lds_bytes) {  // helpers cut the chains they run, and run cuts
-    V.rq = d->rq;
-    V.rq_cap = d->rq_cap;
-  }
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
@@ -1374,11 +1334,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
         pushed += bx[b1::kMigPush] < V.mig_cap / b1::kMigBoxes ? bx[b1::kMigPush] : V.mig_cap / b1::kMigBoxes;
         popped += bx[b1::kMigPop];
       }
-      uint32_t rs[2] = {0u, 0u};
-      HIP_OK(hipMemcpy(rs, d->status + 4, sizeof rs, hipMemcpyDeviceToHost));
-      fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u; re-cut requests %u "
-              "popped %u, cuts %u declined %u (scene totals)\n", mw[b1::kMigHelpers], (unsigned long long)pushed,
-              (unsigned long long)popped, mw[b1::kMigDone], mw[b1::kMigRqPush], mw[b1::kMigRqPop], rs[0], rs[1]);
+      fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u\n", mw[b1::kMigHelpers],
+              (unsigned long long)pushed, (unsigned long long)popped, mw[b1::kMigDone]);
     }
   }
   hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 4 + 1 < 2048 ? npix / 4 + 1 : 2048)), dim3(256), 0, st,
@@ -1388,8 +1345,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   // continuation items (normally none: the launch exits at once)
   b1::Book1View C = V;
   C.n_coop = nullptr;
-  C.rq = nullptr;  // (continuation items are whole pixels: nothing to cut)
-  C.recut_lanes = 0;
   C.ch_cont = d->ch_cont;
   C.ch_n_cont = d->ch_cnt + kCnCont;
   C.mig_epoch = ++d->mig_epoch;
@@ -1498,8 +1453,10 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
 static int pick_mode(const rt_device_scene *d, int64_t npix) {
   const Config &cfg = d->cfg;
   const int spp = d->view.cam.spp;
-  const bool chain_ok = cfg.lpt && spp >= 4 * cfg.lpt_spp && spp >= 2 * cfg.chain_min_seg && npix >= 4096 &&
-                        d->view.cam.max_depth >= 1;
+  // (the pre-pass at most at the frame's spp; RT_LPT_SPP = spp is the diagnostic "exact stream lengths"
+  // plan of scripts/gpu_tail_data.sh)
+  const bool chain_ok = cfg.lpt && spp >= 64 && cfg.lpt_spp <= spp && spp >= 2 * cfg.chain_min_seg &&
+                        npix >= 4096 && d->view.cam.max_depth >= 1;
   if (cfg.mode == kModeChain) return chain_ok ? kModeChain : kModeLane;
   if (cfg.mode == kModeLane) return kModeLane;
   // auto: the chain render whenever it applies (measured ahead of the lane kernel at every N, from
@@ -1804,24 +1761,7 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
       r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len;
     }
   }
-  // then the dynamic segments (run-time re-cuts, run by helper waves): whole-wave flag 2
-  size_t k = n_items;
-  std::vector<uint32_t> split(c[kCnSplit]);
-  HIP_OK(hipMemcpy(split.data(), d->ch_split, split.size() * 4, hipMemcpyDeviceToHost));
-  for (uint32_t p : split) {
-    const b1::ChainPx &P = px[p];
-    for (uint32_t t = P.K; t < P.K + (P.kd & 0xffu) && P.end0 + t < n_seg; t++, k++) {
-      if ((int64_t)k >= max_rows) continue;
-      const uint64_t w = seg[P.end0 + t];
-      uint32_t *r = rows + 16 * k;
-      memset(r, 0, 16 * sizeof(uint32_t));
-      r[0] = p, r[1] = t, r[2] = P.K, r[3] = 2u;
-      r[4] = sgt[2 * (P.end0 + t)], r[5] = sgt[2 * (P.end0 + t) + 1];
-      r[6] = b1::end_n(w);
-      r[7] = ((w & b1::kEndEnded) && !(w & b1::kEndNoLink) ? 1u : 0u) | ((w & b1::kEndEnded) ? 2u : 0u);
-      r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len, r[11] = draws[p], r[12] = costs[p];
-    }
-  }
+  const size_t k = n_items;
   return (int64_t)k;
 }
 
@@ -1841,11 +1781,11 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
              : d->general && d->view.pre && d->cfg.gen_batch ? ", true" : d->general ? ", false" : "");
     return buf;
   }
-  const int mode = pick_mode(d, (int64_t)d->width * d->height);
+  const int64_t npix = (int64_t)d->width * d->height;
+  const int mode = pick_mode(d, npix);
   const char *lds = d->b1_lds_bytes ? "true" : "false";
-  if (mode == kModeChain)  // (every template argument, as rocprofv3 demangles the name: kLds, kRecut, kOcc)
-    snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %s, %d>", lds, d->cfg.recut ? "true" : "false",
-             d->cfg.recut ? 5 : d->chain_occ);
+  if (mode == kModeChain)  // (every template argument, as rocprofv3 demangles the name: kLds, kOcc)
+    snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %d>", lds, chain_occupancy(d, npix));
   else
     snprintf(buf, sizeof buf, "rt_book1_kernel<%s>", lds);
   return buf;

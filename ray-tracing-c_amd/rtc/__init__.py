@@ -22,6 +22,9 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # ray-tra
 # RTC_LIB: an alternative build of the same library (same-box A/B timing of two builds; tests and
 # bench use the in-tree library)
 LIB_PATH = os.path.abspath(os.environ.get("RTC_LIB") or os.path.join(PKG_DIR, "librtc_amd.so"))
+# the diagnostic build of the same sources (-DRT_DIAG): also reads the A/B switches, timeline and
+# fault-injection variables; tests select it with use_diag()
+DIAG_PATH = os.path.join(PKG_DIR, "librtc_amd_diag.so")
 
 # rt_feature_bits (include/rt_flat.h)
 FEAT_BVH, FEAT_QUAD, FEAT_XFORM, FEAT_MEDIUM = 1, 2, 4, 8
@@ -75,7 +78,8 @@ assert ctypes.sizeof(RtCamera) == 128
 assert RtFlatScene.n_image_bytes.offset == 192
 
 
-_lib = None
+_libs = {}          # loaded libraries by path
+_current = LIB_PATH
 _subst_dir = None
 
 
@@ -106,14 +110,35 @@ def _init_torch_runtime_first() -> None:
         pass
 
 
+class use_diag:
+    """Context manager: objects created inside it use the diagnostic build (librtc_amd_diag.so), which
+    reads the A/B switches (RT_MODE, RT_BOOK1_LDS, RT_CHAIN_MARGIN, RT_FAULT_MIG_DROP ...) the product
+    library ignores.  Both libraries can be loaded in one process (each keeps its own symbols)."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+
+    def __enter__(self):
+        global _current
+        self._prev = _current
+        if self.on:
+            _current = DIAG_PATH
+        return self
+
+    def __exit__(self, *exc):
+        global _current
+        _current = self._prev
+        return False
+
+
 def lib() -> ctypes.CDLL:
-    """Load librtc_amd.so (built by ``make -C ray-tracing-c_amd``)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RtcError(f"{LIB_PATH} not built: run `make -C ray-tracing-c_amd` (or __graft_entry__.build())")
+    """Load librtc_amd.so (built by ``make -C ray-tracing-c_amd``), or the diagnostic build inside use_diag()."""
+    path = _current
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RtcError(f"{path} not built: run `make -C ray-tracing-c_amd` (or __graft_entry__.build())")
         _init_torch_runtime_first()
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         P = POINTER(RtFlatScene)
         L.rt_scene_preset.argtypes = [c_int, c_int, c_int, c_int]
         L.rt_scene_preset.restype = P
@@ -145,12 +170,14 @@ def lib() -> ctypes.CDLL:
         L.rt_last_error.restype = c_char_p
         L.rt_abi_version.restype = c_int
         L.rt_build_id.restype = c_char_p
-        _lib = L
-    return _lib
+        L.rt_scene_chain_diag.argtypes = [c_void_p, c_void_p, c_int64]
+        L.rt_scene_chain_diag.restype = c_int64
+        _libs[path] = L
+    return _libs[path]
 
 
-def last_error() -> str:
-    return (lib().rt_last_error() or b"").decode(errors="replace")
+def last_error(L=None) -> str:
+    return ((L or lib()).rt_last_error() or b"").decode(errors="replace")
 
 
 def build_id() -> str:
@@ -161,9 +188,10 @@ def build_id() -> str:
 class Scene:
     """An owned rt_flat_scene (host memory)."""
 
-    def __init__(self, ptr):
+    def __init__(self, ptr, L=None):
+        self._L = L or lib()
         if not ptr:
-            raise RtcError(f"scene construction failed: {last_error()}")
+            raise RtcError(f"scene construction failed: {last_error(self._L)}")
         self._ptr = ptr
 
     @classmethod
@@ -182,7 +210,8 @@ class Scene:
         if image_dir is None and substitute_earth and int(scene_id) in (3, 7):
             image_dir = substitute_dir()
         d = image_dir.encode() if image_dir is not None else None
-        return cls(lib().rt_scene_preset_in(int(scene_id), int(width), int(spp), int(max_depth), d))
+        L = lib()
+        return cls(L.rt_scene_preset_in(int(scene_id), int(width), int(spp), int(max_depth), d), L)
 
     @property
     def ptr(self):
@@ -217,7 +246,7 @@ class Scene:
 
     def close(self):
         if self._ptr:
-            lib().rt_flat_free(self._ptr)
+            self._L.rt_flat_free(self._ptr)
             self._ptr = None
 
     def __del__(self):
@@ -234,9 +263,10 @@ def device_count() -> int:
 def render(scene: Scene, n_gpus: int = 1) -> np.ndarray:
     """Whole frame on the GPU(s) into a host (H, W, 3) uint8 array (what Camera_render does)."""
     out = np.empty((scene.height, scene.width, 3), dtype=np.uint8)
-    rc = lib().rt_render(scene.ptr, int(n_gpus), out.ctypes.data)
+    L = lib()
+    rc = L.rt_render(scene.ptr, int(n_gpus), out.ctypes.data)
     if rc != 0:
-        raise RtcError(f"rt_render failed: {last_error()}")
+        raise RtcError(f"rt_render failed: {last_error(L)}")
     return out
 
 
@@ -250,34 +280,44 @@ class DeviceScene:
     def __init__(self, scene: Scene, device: int = 0):
         self.scene = scene
         self.device = device
-        self._h = lib().rt_scene_upload(scene.ptr, int(device))
+        self._L = lib()
+        self._h = self._L.rt_scene_upload(scene.ptr, int(device))
         if not self._h:
-            raise RtcError(f"rt_scene_upload failed: {last_error()}")
+            raise RtcError(f"rt_scene_upload failed: {last_error(self._L)}")
 
     def render_rows_async(self, row0: int, row_stride: int, n_rows: int, d_out_ptr: int, stream_ptr: int = 0):
-        rc = lib().rt_render_rows_async(self._h, int(row0), int(row_stride), int(n_rows),
-                                        c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
+        rc = self._L.rt_render_rows_async(self._h, int(row0), int(row_stride), int(n_rows),
+                                          c_void_p(int(d_out_ptr)), c_void_p(int(stream_ptr)))
         if rc != 0:
-            raise RtcError(f"rt_render_rows_async failed: {last_error()}")
+            raise RtcError(f"rt_render_rows_async failed: {last_error(self._L)}")
 
     def check(self):
         """Wait for this scene's launches and raise RtcError if any work item never finished
         (rt_scene_check): the rows written are then not a valid frame."""
-        if lib().rt_scene_check(self._h) != 0:
-            raise RtcError(f"rt_scene_check: {last_error()}")
+        if self._L.rt_scene_check(self._h) != 0:
+            raise RtcError(f"rt_scene_check: {last_error(self._L)}")
 
     def last_launch_ms(self) -> float:
         """Duration of the last frame launch (excludes the cost pre-pass); call after it completed."""
-        return float(lib().rt_scene_last_launch_ms(self._h))
+        return float(self._L.rt_scene_last_launch_ms(self._h))
 
     @property
     def kernel_name(self) -> str:
         """The kernel rt_render_rows_async launches for this scene (rocprofv3's name for it)."""
-        return (lib().rt_scene_kernel(self._h) or b"").decode()
+        return (self._L.rt_scene_kernel(self._h) or b"").decode()
+
+    def chain_diag(self, max_rows: int) -> np.ndarray:
+        """Item rows of the last chain launch (rt_hip.h: rt_scene_chain_diag; diagnostic build with
+        RT_PX_TIME=1 at upload): (items, 16) uint32."""
+        rows = np.zeros((max_rows, 16), np.uint32)
+        m = self._L.rt_scene_chain_diag(self._h, rows.ctypes.data, int(max_rows))
+        if m < 0:
+            raise RtcError(f"rt_scene_chain_diag: {last_error(self._L)}")
+        return rows[:min(m, max_rows)]
 
     def close(self):
         if self._h:
-            lib().rt_scene_release(self._h)
+            self._L.rt_scene_release(self._h)
             self._h = None
 
     def __del__(self):
@@ -285,6 +325,36 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+
+def box_identity(device: int = 0) -> dict:
+    """Which machine and GPU a measurement ran on (chain-mode timings differ between
+    boxes, so every probe and bench line names its box): host name, the GPU's UUID and PCI location
+    as the HIP runtime reports them, and the board serial from rocm-smi when it answers."""
+    import socket
+    import subprocess
+
+    ident = {"host": socket.gethostname()}
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            p = torch.cuda.get_device_properties(device)
+            ident["gpu_uuid"] = str(getattr(p, "uuid", ""))
+            ident["pci"] = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:" \
+                           f"{getattr(p, 'pci_device_id', 0):02x}"
+        except Exception:  # no GPU visible: host only
+            pass
+    try:
+        out = subprocess.run(["rocm-smi", "--showserial", "--json"], capture_output=True, text=True, timeout=20).stdout
+        import json
+
+        cards = json.loads(out) if out.strip().startswith("{") else {}
+        serials = [v.get("Serial Number") for v in cards.values() if isinstance(v, dict) and v.get("Serial Number")]
+        if serials:
+            ident["smi_serial"] = serials[0] if len(serials) == 1 else serials
+    except Exception:
+        pass
+    return ident
 
 
 def rows_of(height: int, rank: int, world: int):

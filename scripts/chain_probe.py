@@ -1,7 +1,7 @@
-"""Timeline of one chain launch (RT_PX_TIME=1 diagnostic): every work item's start / end, by kind
-(unsplit lane pixel, lane segment, whole-wave segment), and the items that finish last.
+"""Timeline of one chain launch (RT_PX_TIME=1 diagnostic of the diagnostic build librtc_amd_diag.so):
+every work item's start / end, by kind (unsplit lane pixel, lane segment, whole-wave segment), and the
+items that finish last.
     python scripts/chain_probe.py WORLD RANK [SPP]       (RT_* knobs from the environment)"""
-import ctypes
 import os
 import sys
 import time
@@ -14,8 +14,9 @@ import rtc  # noqa: E402
 
 world, rank = int(sys.argv[1]), int(sys.argv[2])
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
-sc = rtc.Scene.preset(1, 1200, spp, 50)
-ds = rtc.DeviceScene(sc, 0)
+with rtc.use_diag():
+    sc = rtc.Scene.preset(1, 1200, spp, 50)
+    ds = rtc.DeviceScene(sc, 0)
 row0, stride, n = rtc.rows_of(sc.height, rank, world)
 buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream()
@@ -24,22 +25,17 @@ for _ in range(2):
     ds.render_rows_async(row0, stride, n, buf.data_ptr(), st.cuda_stream)
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
-L = rtc.lib()
-L.rt_scene_chain_diag.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
-L.rt_scene_chain_diag.restype = ctypes.c_int64
-cap = sc.width * sc.height * 64
-rows = np.zeros((cap, 16), np.uint32)
-m = L.rt_scene_chain_diag(ds._h, rows.ctypes.data, cap)
-assert m >= 0, rtc.last_error()
-r = rows[:m].astype(np.int64)
+rows = ds.chain_diag(n * sc.width * 64)
+m = len(rows)
+r = rows.astype(np.int64)
 t0 = r[:, 4].min()
 start = (r[:, 4] - t0) / 1e5  # wall_clock64: 100 MHz -> ms
 end = (r[:, 5] - t0) / 1e5
+print(f"build={ds._L.rt_build_id().decode()} (diag) box={rtc.box_identity(0)}", flush=True)
 print(f"world={world} rank={rank} ms={t * 1e3:.1f} kernel_ms={ds.last_launch_ms():.1f} items={m} "
       f"last_end={end.max():.1f} ms", flush=True)
 kinds = {"unsplit lane": (r[:, 2] == 1) & (r[:, 3] == 0), "unsplit wave": (r[:, 2] == 1) & (r[:, 3] == 1),
-         "segment lane": (r[:, 2] > 1) & (r[:, 3] == 0), "segment wave": (r[:, 2] > 1) & (r[:, 3] == 1),
-         "re-cut (dyn)": r[:, 3] == 2}
+         "segment lane": (r[:, 2] > 1) & (r[:, 3] == 0), "segment wave": (r[:, 2] > 1) & (r[:, 3] == 1)}
 for name, k in kinds.items():
     if k.any():
         d = end[k] - start[k]
@@ -76,6 +72,6 @@ print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, f
 for q in last:
     print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]} {r[q, 8]}:{r[q, 9]} {r[q, 10]} {r[q, 11]}")
 if os.environ.get("CHAIN_ROWS"):  # the item rows for offline analysis (uint32, compressed)
-    np.savez_compressed(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", f"chain_rows_{world}_{rank}.npz"),
-                        rows=rows[:m])
+    np.savez_compressed(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", f"chain_rows_{world}_{rank}{os.environ.get('CHAIN_TAG', '')}.npz"),
+                        rows=rows)
 ds.close()

@@ -35,6 +35,7 @@ def time_rows(row0, stride, n, reps=2):
     return best, kbest
 
 
+print(f"build={rtc.build_id()} box={rtc.box_identity(0)}", flush=True)
 t1, k1 = time_rows(0, 1, sc.height)
 full = last
 print(f"world=1 ms={t1 * 1e3:.1f} kernel_ms={k1:.1f} Msamples/s={sc.width * sc.height * spp / t1 / 1e6:.0f}", flush=True)

@@ -3,12 +3,12 @@
 // chain_record, the same code the kernel compiles) on the CPU with AddressSanitizer, over a small
 // frame of a Book-1 scene, with adversarial plans: random segment counts, stream-length estimates
 // off by up to 2x, tiny record lists (forcing continuations) and a random interleaving of the chains
-// (random start delays, one sample per scheduling step), with run-time re-cuts (RecutReq) requested by
-// random last segments and published by a simulated helper at random times, with random cut points.
-// Then the fold and the continuations, as chain_fold_kernel and the continuation launch do.  tests/test_kernel_logic.py compares the image
+// (random start delays, one sample per scheduling step).  Then the fold and the continuations, as chain_fold_kernel and the continuation launch do.  tests/test_kernel_logic.py compares the image
 // with the oracle: the protocol must be exact whatever the plan and the timing.
 // It is not part of the product and is never linked into librtc_amd.so.
-//   chain_sim <scene> <width> <spp> <depth> <out.rgb> <seed> <kmin> <kmax> <margin> <slack> [recut 0/1]
+//   chain_sim <scene> <width> <spp> <depth> <out.rgb> <seed> <kmin> <kmax> <margin> <slack> [pad]
+// pad > 1: stream-length estimates off by up to 2x are then spread over pad x the estimate (the
+// planner's padded plan for many-segment pixels: segments past the true stream end).
 #include "../../ray-tracing-c_amd/csrc/rt_book1.h"
 #include "../../include/rt_hip.h"
 
@@ -35,7 +35,6 @@ struct Chain {
   f3 acc;
   int start_at;  // scheduling step before which it does not run
   bool done;
-  bool wave;     // started by a (simulated) helper: a dynamic segment
 };
 
 // one sample of pixel (i, j) from the chain's rng state (Camera_render's loop body)
@@ -74,6 +73,7 @@ int main(int argc, char **argv) {
   const int kmin = atoi(argv[7]), kmax = atoi(argv[8]);
   const float margin = (float)atof(argv[9]);
   const uint32_t slack = (uint32_t)atoi(argv[10]);
+  const double pad = argc > 11 ? atof(argv[11]) : 1.0;
   const void *arrays[13] = {s->bvh,        s->spheres,  s->quads,     s->lists,  s->list_items,
                             s->translates, s->rotates,  s->media,     s->materials, s->textures,
                             s->images,     s->perlins,  s->image_bytes};
@@ -96,21 +96,21 @@ int main(int argc, char **argv) {
     Pcg32 g;
     g.seed((uint64_t)(17 + p / W), (uint64_t)(23 + p % W));
     for (int q = 0; q < 4; q++) (void)sample(view, p, g);
-    const double est = (double)g.n / 4.0 * spp * (0.5 + 1.5 * (rnd() % 1000) / 1000.0);
+    const double est = (double)g.n / 4.0 * spp * (0.5 + 1.5 * (rnd() % 1000) / 1000.0) * (pad > 1.0 ? pad : 1.0);
     uint32_t seg_len = ((uint32_t)(est / K) + 1u) & ~1u;
     if (seg_len < 2) K = 1;
     if (K > 1) {
       b1::ChainPx &P = px[p];
       P.K = (uint32_t)K;
       P.seg_len = seg_len;
-      P.cap = (uint32_t)ceilf(margin * (float)spp / (float)K) + slack;
+      P.cap = (uint32_t)ceilf(fminf(margin, (float)K) * (float)spp / (float)K) + slack;  // (as chain_plan_kernel)
       P.cap_last = (rnd() & 1) ? P.cap : (uint32_t)spp + slack;  // (the planner's, or a short one)
       P.rec0 = rec;
       rec += (uint32_t)(K - 2) * P.cap + P.cap_last;
       P.end0 = (uint32_t)seg.size();
       P.check = (uint32_t)(3 * (spp / K) / 4);
-      P.kd = 0u;
-      for (uint32_t k = 0; k < (uint32_t)K + b1::kDynMax; k++) seg.push_back(0ull);
+      P.pad = 0u;
+      for (uint32_t k = 0; k < (uint32_t)K; k++) seg.push_back(0ull);
       split.push_back((uint32_t)p);
     }
     for (int k = 0; k < K; k++) {
@@ -126,22 +126,14 @@ int main(int argc, char **argv) {
         c.g.skip((uint32_t)k * seg_len);
         if (k + 1 < K) c.tc = (uint32_t)(k + 1) << 24, c.st = (uint32_t)(k + 1) * seg_len;
       }
-      c.wave = false;
       c.start_at = (int)(rnd() % 64u);
       c.done = false;
       chains.push_back(c);
     }
   }
-  const bool recut = argc > 11 && atoi(argv[11]) != 0;
-  const uint32_t cap_dyn = (uint32_t)spp + slack;
-  const size_t rec_room = rec + (recut ? (size_t)split.size() * b1::kDynMax * cap_dyn / 4 : 0);  // (cuts may run out: fine)
-  col.assign(rec_room, make_float4(0, 0, 0, 0));
-  endw.assign(rec_room, b1::kRecFill);
-  std::vector<b1::SegDyn> sd(seg.size(), b1::SegDyn{0u, 0u, 0u, 0u});
+  col.assign(rec, make_float4(0, 0, 0, 0));
+  endw.assign(rec, b1::kRecFill);
   std::vector<uint32_t> mig(b1::kMigWords, 0u);
-  const uint32_t filled = (uint32_t)rec_room;
-  std::vector<b1::RecutReq> rq(4 * split.size() + 16);
-  unsigned long long rec_count = rec;
   b1::Book1View V;
   memset(&V, 0, sizeof V);
   V.S = view;
@@ -150,18 +142,8 @@ int main(int argc, char **argv) {
   V.ch_col = col.data();
   V.ch_end = endw.data();
   V.ch_acc0 = acc0.data();
-  V.ch_sd = sd.data();
   V.mig = mig.data();
   V.mig_epoch = 1u;
-  V.rec_count = &rec_count;
-  V.rec_filled = &filled;
-  V.recut_min = 4u;
-  V.recut_slack = slack;
-  if (recut) {
-    V.rq = rq.data();
-    V.rq_cap = (uint32_t)rq.size();
-  }
-  long cuts = 0, requests = 0;
   // interleaved execution: a random live chain takes one step (boundary, then one sample)
   std::vector<int> live;
   for (int c = 0; c < (int)chains.size(); c++) live.push_back(c);
@@ -179,35 +161,6 @@ int main(int argc, char **argv) {
       live[at] = live.back();
       live.pop_back();
       continue;
-    }
-    // a chain asks for a cut (the kernels: in the launch's tail) at a random point of its remaining
-    // draws; a server publishes requests at random times
-    if (V.rq && (rnd() & 7u) == 0u && (c.s & 3u) == 0u) {
-      V.recut_frac = 0.02f + 0.96f * (float)(rnd() % 1000u) / 1000.0f;
-      const uint32_t before = mig[b1::kMigRqPush];
-      b1::recut_ask(V, (uint32_t)c.pix, c.seg, c.g.n, c.s, true, c.tc);
-      requests += mig[b1::kMigRqPush] - before;
-    }
-    int req = -1;
-    if (V.rq && (rnd() & 3u) == 0u && (req = b1::recut_pop(V)) >= 0) {
-      const b1::RecutReq r = rq[(uint32_t)req];
-      const uint32_t t = b1::recut_publish(V, r);
-      if (t) {
-        cuts++;
-        Chain d;
-        d.pix = (int32_t)r.pix;
-        d.seg = t;
-        d.g.seed((uint64_t)(17 + r.pix / W), (uint64_t)(23 + r.pix % W));
-        b1::chain_start(V, r.pix, t, d.g, d.tc, d.st);
-        d.s = 0;
-        d.acc = mk(0.0f, 0.0f, 0.0f);
-        d.start_at = (int)(rnd() % 16u);
-        d.done = false;
-        d.wave = true;
-        chains.push_back(d);
-        live.push_back((int)chains.size() - 1);
-        continue;  // (c may have moved with the vector)
-      }
     }
     const f3 color = sample(view, c.pix, c.g);
     samples++;
@@ -229,9 +182,9 @@ int main(int argc, char **argv) {
     }
     f3 acc = mk(acc0[p].x, acc0[p].y, acc0[p].z);
     uint32_t total = b1::end_n(w), t = b1::end_t(w), c = b1::end_c(w);
-    uint32_t o = c == 0 ? b1::seg_start(V, P, t) : endw[b1::rec_index(V, P, t, c - 1)];
+    uint32_t o = c == 0 ? b1::seg_start(P, t) : endw[b1::rec_index(P, t, c - 1)];
     for (;;) {
-      if (t == 0 || t >= P.K + b1::kDynMax) {
+      if (t == 0 || t >= P.K) {
         fprintf(stderr, "pixel %u: bad link %u\n", p, t);
         return 3;
       }
@@ -242,7 +195,7 @@ int main(int argc, char **argv) {
       }
       const uint32_t n = b1::end_n(w);
       for (uint32_t q = c; q < n && total < (uint32_t)spp; q++) {
-        const float4 r = col[b1::rec_index(V, P, t, q)];
+        const float4 r = col[b1::rec_index(P, t, q)];
         acc = add(acc, mk(r.x, r.y, r.z));
         o = b1::f2u(r.w);
         total++;
@@ -262,8 +215,8 @@ int main(int argc, char **argv) {
   FILE *f = fopen(argv[5], "wb");
   fwrite(img.data(), 1, img.size(), f);
   fclose(f);
-  printf("%d %d split=%zu chains=%zu samples=%ld (x%.3f) continuations=%d requests=%ld cuts=%ld\n", W, H, split.size(),
-         chains.size(), samples, (double)samples / ((double)npix * spp), n_cont, requests, cuts);
+  printf("%d %d split=%zu chains=%zu samples=%ld (x%.3f) continuations=%d\n", W, H, split.size(),
+         chains.size(), samples, (double)samples / ((double)npix * spp), n_cont);
   rt_flat_free(s);
   return 0;
 }

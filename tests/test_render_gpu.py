@@ -206,31 +206,34 @@ def test_cli_rt_main_matches_golden(manifest, tmp_path):
     assert data[:168] == open(os.path.join(ROOT, "tests", "golden", "tiff_header.bin"), "rb").read()
 
 
+# Tests that select a path or force a fallback by RT_* switches use the diagnostic build
+# (librtc_amd_diag.so, -DRT_DIAG: the product library reads only the planner parameters).
 CHAIN = {"RT_MODE": "chain", "RT_LPT_SPP": "1", "RT_CHAIN_MIN_SEG": "4"}
+SPLIT = {**CHAIN, "RT_CHAIN_BETA": "0.001"}  # every pixel split as far as allowed
 
 
 @pytest.mark.parametrize("env", [
-    {}, {"RT_BOOK1": "0"}, {"RT_BOOK1": "0", "RT_GENERAL": "0"}, {"RT_BOOK1_LDS": "0"},
-    {"RT_MODE": "lane"}, {"RT_MODE": "lane", "RT_BOOK1_LDS": "0"},
-    {"RT_SHADE_BATCH": "1"}, {"RT_SHADE_BATCH": "64", "RT_BOOK1_LDS": "0"},
-    CHAIN,                                                         # the chain render, planned
-    {**CHAIN, "RT_CHAIN_BETA": "0.001"},                           # every pixel split as far as allowed
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_KMAX": "64"},    # many short segments (lanes)
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_KMAX": "1"},     # every split pixel on whole waves
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},  # continuations
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_CHAIN_MB": "1"},       # out of records: pixels stay whole
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BOOK1_LDS": "0"},      # global-memory scene, lanes only
-    {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_BF": "0", "RT_CHAIN_KMAX": "2"},
-    {**CHAIN, "RT_CHAIN_OCC": "3"}, {**CHAIN, "RT_CHAIN_OCC": "4"}, {**CHAIN, "RT_CHAIN_OCC": "5"},  # every occupancy
+    {},                                                       # the default plan (chain at 100 spp, lanes at 16)
+    {"RT_MODE": "lane"},                                      # the lane kernel (low spp, small launches)
+    {"RT_BOOK1_LDS": "0", "RT_MODE": "lane"},                 # scenes whose items exceed 64 KiB: global memory
+    {**SPLIT, "RT_BOOK1_LDS": "0"},                           #   ... chain render on them (lanes only)
+    CHAIN, SPLIT,                                             # the chain render, planned / fully split
+    {**SPLIT, "RT_CHAIN_KMAX": "1"},                          # every split pixel on whole waves
+    {**SPLIT, "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},  # lists that fill up: continuations
+    {**SPLIT, "RT_CHAIN_MB": "1"},                            # out of records: pixels stay whole
+    {**CHAIN, "RT_CHAIN_OCC": "3"}, {**CHAIN, "RT_CHAIN_OCC": "5"},  # both chain kernel occupancies
+    {"RT_BOOK1": "0"},                                        # the general kernel on Book-1 scenes
 ])
 @pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
-def test_book1_fast_path_and_general_kernel_agree(manifest, name, env, monkeypatch):
-    """Book-1 scenes run on the persistent fast kernel (LDS or global geometry) unless RT_BOOK1=0
-    selects the general kernel; every variant must reproduce the reference frame."""
+def test_book1_shipped_paths_reproduce_reference(manifest, name, env, monkeypatch):
+    """Every path the product takes for Book-1 scenes -- lane or chain kernel, LDS or global-memory
+    items, split / whole-wave / continuation / unsplit-fallback items, both occupancies -- and the
+    general kernel on the same scenes, forced on small goldens: each must reproduce the reference frame."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"][name]
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    with rtc.use_diag():
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), f"{name} {env}")
 
 
@@ -249,7 +252,7 @@ def test_book1_deep_paths_spill(monkeypatch):
 
 @pytest.mark.parametrize("env", [{}, {"RT_CHAIN_BETA": "0.002"}, {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_KMAX": "64"},
                                  {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},
-                                 {"RT_CHAIN_OCC": "3"}, {"RT_CHAIN_OCC": "4"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"}])
+                                 {"RT_CHAIN_OCC": "3"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"}])
 def test_chain_render_north_star_scene(manifest, env, monkeypatch):
     """Chain render (rt_book1.h: ChainPx) forced on the Book-1 final scene at full size: pixel
     streams cut into segments, chains coupling on equal stream offsets, the fold and the
@@ -260,23 +263,24 @@ def test_chain_render_north_star_scene(manifest, env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    with rtc.use_diag():
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"], env
 
 
-@pytest.mark.parametrize("env", [{"RT_GEN_PRE": "0"}, {"RT_GEN_BATCH": "0"}, {"RT_GEN_BATCH": "1", "RT_GEN_STEPS": "1"},
-                                 {"RT_GEN_BATCH": "64", "RT_GEN_STEPS": "32"}, {"RT_LPT": "0"}, {"RT_GEN_LDS": "0"},
-                                 {"RT_GEN_LDS": "7"}, {"RT_GEN_LDS": "2048"}, {"RT_GEN_FLAT": "2"},
-                                 {"RT_GEN_FLAT": "1"}, {"RT_GEN_FLAT": "6"}, {"RT_GEN_RARE": "1"}, {"RT_GEN_RARE": "64", "RT_GEN_STEPS": "3"}])
+@pytest.mark.parametrize("env", [{"RT_GEN_BIG": "0"}, {"RT_GEN_BIG": "0", "RT_GEN_LDS": "0"},
+                                 {"RT_GEN_BIG": "0", "RT_GEN_LDS": "7"}, {"RT_GEN_PERLIN_LDS": "0"}])
 @pytest.mark.parametrize("name", ["s5_200x112_16spp_d50", "s6_200x200_16spp_d50", "s7_200x200_8spp_d50"])
-def test_general_path_variants(manifest, name, env, monkeypatch):
-    """The general kernel's trace (preorder scan or stack; straight-line or branched common entries;
-    rare entries deferred or not) and loop (batched or one bounce per iteration) variants must all
-    reproduce the reference frames (transforms, media, lights)."""
+def test_general_path_shipped_variants(manifest, name, env, monkeypatch):
+    """The general kernel as it ships for scenes whose preorder exceeds one workgroup's LDS (256-thread
+    workgroups, the preorder's top staged in LDS or none of it) and without the Perlin tables in LDS:
+    each must reproduce the reference frames (transforms, media, lights).  (The default, whole
+    preorder in one 768-thread workgroup's LDS, is test_gpu_matches_reference_render.)"""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"][name]
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    with rtc.use_diag():
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), f"{name} {env}")
 
 
@@ -315,7 +319,8 @@ def test_migration_helpers_leaving_early_lose_no_work(manifest, wait_us, monkeyp
     for k, v in {**MIGRATE, "RT_MIG_WAIT_US": wait_us}.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"]["s1_300x168_16spp_d50"]
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    with rtc.use_diag():
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), f"migration, helpers wait {wait_us} us")
 
 
@@ -326,12 +331,17 @@ def test_lost_work_item_is_reported_not_rendered_silently(manifest, monkeypatch)
     for k, v in {**MIGRATE, "RT_MIG_WAIT_US": "2000", "RT_FAULT_MIG_DROP": "1"}.items():
         monkeypatch.setenv(k, v)
     e = manifest["renders"]["s1_300x168_16spp_d50"]
-    with pytest.raises(rtc.RtcError, match="never finished"):
-        rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
-    # the status is per scene and cleared by the check: a clean render afterwards succeeds
-    monkeypatch.delenv("RT_FAULT_MIG_DROP")
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    with rtc.use_diag():
+        with pytest.raises(rtc.RtcError, match="never finished"):
+            rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+        # the status is per scene and cleared by the check: a clean render afterwards succeeds
+        monkeypatch.delenv("RT_FAULT_MIG_DROP")
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     _check(img, golden_image(e), "after the fault")
+    # the product library has no fault injection: the same variables render the exact frame
+    monkeypatch.setenv("RT_FAULT_MIG_DROP", "1")
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    _check(img, golden_image(e), "product library ignores RT_FAULT_MIG_DROP")
 
 
 def test_rehearsed_eight_device_render_threads(manifest, monkeypatch):
@@ -370,31 +380,3 @@ def test_dropin_reference_main_on_eight_rehearsed_devices(manifest, tmp_path):
     data = open(os.path.join(str(tmp_path), "output.tiff"), "rb").read()
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
     assert hashlib.sha256(data[168:]).hexdigest() == e["sha256"]
-
-
-# Run-time re-cuts (rt_book1.h: RecutReq; opt-in RT_RECUT=1): in a chain launch's tail a lane hands an
-# idle lane of its wave a cut of its own chain, and helper waves cut the chains they run.
-@pytest.mark.parametrize("env", [
-    {"RT_RECUT": "1"},
-    {**CHAIN, "RT_RECUT": "1", "RT_RECUT_MIN": "4"},
-    {**CHAIN, "RT_RECUT": "1", "RT_RECUT_MIN": "4", "RT_RECUT_FRAC": "0.1"},
-    {**MIGRATE, "RT_RECUT": "1", "RT_RECUT_MIN": "4", "RT_RECUT_FRAC": "0.9"}])
-@pytest.mark.parametrize("name", ["s0_400x225_100spp_d50", "s1_300x168_16spp_d50"])
-def test_recut_chains_reproduce_reference(manifest, name, env, monkeypatch):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    e = manifest["renders"][name]
-    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
-    _check(img, golden_image(e), f"{name} {env}")
-
-
-def test_recut_north_star_eight_shares(manifest, monkeypatch):
-    """The north-star frame as 8 concurrent shares (rt_render, RT_REHEARSE_DEVICES=8) with re-cuts on:
-    the N = 8 tail is where cuts happen; the frame must be the reference's."""
-    e = manifest["renders"].get("s1_1200x675_1000spp_d50")
-    if e is None:
-        pytest.skip("north-star golden not generated (make_golden.py --big)")
-    monkeypatch.setenv("RT_REHEARSE_DEVICES", "8")
-    monkeypatch.setenv("RT_RECUT", "1")
-    img = rtc.render(rtc.Scene.preset(1, 1200, 1000, 50), n_gpus=8)
-    assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"]
