@@ -317,6 +317,8 @@ struct ChainModel {
   int min_seg;          // samples per segment at least
   int width, smooth;    // launch row width; draw estimates averaged over +-smooth pixels of the row
   float est_scale;      // stream length estimate x this
+  float pad;            // pixels of >= pad_k segments: segments of the planned length over pad x the estimate
+  int pad_k;
   uint32_t rec_cap;     // records available
   uint32_t seg_cap;     // end words available
 };
@@ -364,6 +366,14 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
     const double est = dsum / dn * m.ratio * m.est_scale;
     if (K > 1 && est * 2.0 >= 4294967295.0) K = 1;   // u32 offsets
     uint32_t seg_len = K > 1 ? (uint32_t)ceil(est / K) : 0u;
+    // padded plan: the estimate's error lands on the last segment, K times its share of the stream
+    // (DESIGN.md §5), so a pixel of many segments gets more segments of the same length, reaching past
+    // the estimate: the true end falls inside one of them, and those past it stop when the pixel is done
+    if (m.pad > 1.0f && K >= m.pad_k) {
+      const int kp = min(min((int)ceilf((float)K * m.pad), max(m.kmax_lane, m.kmax_wave)), max(K, m.spp / m.min_seg));
+      seg_len = (uint32_t)ceil(est * m.pad / kp);
+      K = kp;
+    }
     seg_len = (seg_len + 1u) & ~1u;  // even: most draw counts are even
     if (seg_len < 2u) K = 1;
     if (K > 1) {
@@ -538,6 +548,8 @@ struct Config {
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
+  float chain_pad = 1.0f;  // padded plan (chain_plan_kernel): off at 1
+  int chain_pad_k = 8;
   float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
   int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
@@ -604,6 +616,8 @@ struct Config {
     c.chain_smooth = env_int("RT_CHAIN_SMOOTH", c.chain_smooth);
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
+    c.chain_pad = env_float("RT_CHAIN_PAD", c.chain_pad);
+    c.chain_pad_k = env_int("RT_CHAIN_PAD_K", c.chain_pad_k);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
     c.chain_occ_px = env_float("RT_CHAIN_OCC_PX", c.chain_occ_px);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
@@ -1262,6 +1276,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.width = V.S.cam.width;
   m.smooth = cfg.chain_smooth;
   m.est_scale = cfg.chain_est;
+  m.pad = cfg.chain_pad;
+  m.pad_k = cfg.chain_pad_k < 2 ? 2 : cfg.chain_pad_k;
   m.kmax_lane = cfg.chain_kmax;
   {  // enough items to give every lane of the grid one: light pixels' 1000-sample chains were the
      // launch's longest items at N = 8 (per-sample overhead, not traversal steps, sets their latency)

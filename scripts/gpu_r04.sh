@@ -41,6 +41,18 @@ if [ -n "${AB:-}" ]; then
 fi
 [ "${S7:-0}" = 1 ] && step s7_bench 300 python bench.py --no-cpu-baseline --scene 7 --width 1000 --steps 1 --warmup 1
 [ "${SHARD:-0}" = 1 ] && step shard 400 python -u scripts/shard_probe.py ${WORLDS:-2,4,8} all 1000
+# SHARD_ENVS="RT_CHAIN_PAD=1.2;...": the shard probe on the diagnostic build under each setting
+if [ -n "${SHARD_ENVS:-}" ]; then
+  IFS=';' read -ra SE <<< "$SHARD_ENVS"
+  for r in $(seq 1 ${ROUNDS:-2}); do
+    for e in "${SE[@]}"; do
+      env RTC_DIAG=1 $e timeout -k 10 400 python -u scripts/shard_probe.py ${WORLDS:-2,4,8} all 1000 > gpurun_out/${TAG}_shard_env.log 2>&1
+      rc=$?
+      echo "== shard [$e] round $r rc=$rc"; grep -E "^world|identical=False|Error" gpurun_out/${TAG}_shard_env.log
+      [ $rc -ne 0 ] && { tail -5 gpurun_out/${TAG}_shard_env.log; exit $rc; }
+    done
+  done
+fi
 for wr in ${PAIRS:-}; do
   w=${wr%%:*}; r=${wr##*:}
   CHAIN_ROWS=1 CHAIN_TAG=_plan step chain_${w}_${r} 300 python -u scripts/chain_probe.py $w $r 1000

@@ -13,8 +13,10 @@ import rtc  # noqa: E402
 worlds = [int(w) for w in sys.argv[1].split(",")]
 ranks_arg = sys.argv[2] if len(sys.argv) > 2 else "0"
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
-sc = rtc.Scene.preset(1, 1200, spp, 50)
-ds = rtc.DeviceScene(sc, 0)
+# RTC_DIAG=1: the diagnostic build (librtc_amd_diag.so), which reads the A/B switches (RT_CHAIN_PAD ...)
+with rtc.use_diag(os.environ.get("RTC_DIAG") == "1"):
+    sc = rtc.Scene.preset(1, 1200, spp, 50)
+    ds = rtc.DeviceScene(sc, 0)
 st = torch.cuda.current_stream()
 
 
@@ -35,7 +37,8 @@ def time_rows(row0, stride, n, reps=2):
     return best, kbest
 
 
-print(f"build={rtc.build_id()} box={rtc.box_identity(0)}", flush=True)
+print(f"build={ds._L.rt_build_id().decode()} box={rtc.box_identity(0)} "
+      f"env={ {k: v for k, v in os.environ.items() if k.startswith('RT_') or k == 'RTC_DIAG'} }", flush=True)
 t1, k1 = time_rows(0, 1, sc.height)
 full = last
 print(f"world=1 ms={t1 * 1e3:.1f} kernel_ms={k1:.1f} Msamples/s={sc.width * sc.height * spp / t1 / 1e6:.0f}", flush=True)
