@@ -24,6 +24,7 @@ struct GeneralView {
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
   int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
+  int32_t wait_min;          // kBatch: a lane at a sphere / quad waits until this many stepping lanes are at one (1: never)
   int32_t flat;              // kBatch: common entries as one straight-line block (pre_common) plus up to
                              // flat - 1 box entries in the same step (RT_GEN_FLAT, >= 1)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
@@ -357,12 +358,24 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
 // only the quad's in-plane test (its record: measured no faster when loaded up front) and the
 // sphere's out-of-range fallback branch.
 // Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
+// wait_min > 1: a lane at a sphere (a quad) waits on its entry while lanes sit at boxes, until at least
+// wait_min of the stepping lanes are at spheres (quads) -- the block then runs for more lanes at once
+// (Book-1's leaf wait, rt_book1.h trav_step_v9); a lane's own entry sequence is unchanged.  The caller
+// calls this with exec = the stepping lanes (the ballots count those).
 template <int F>
 RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin, float4 q0, float4 q1,
-                     int extra = 0) {
+                     int extra = 0, int wait_min = 1) {
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
   const int kind = rt_ref_kind(ref);
   const f3 o = T.o, d = T.d;
+  const uint64_t m_sph = __ballot(kind == RT_KIND_SPHERE), m_quad = (F & RT_FEAT_QUAD) ? __ballot(kind == RT_KIND_QUAD) : 0ull;
+  bool run_sph = m_sph != 0ull, run_quad = m_quad != 0ull;
+  if (wait_min > 1) {  // (wave-uniform)
+    const bool boxes = __ballot(kind == RT_KIND_BVH) != 0ull;
+    run_sph = run_sph && (!boxes || (int)__popcll(m_sph) >= wait_min);
+    run_quad = run_quad && (!boxes || (int)__popcll(m_quad) >= wait_min);
+  }
+  const bool waits = (kind == RT_KIND_SPHERE && !run_sph) || (kind == RT_KIND_QUAD && !run_quad);
   // box: q0 = (lo.x, lo.y, lo.z, hi.x), q1 = (hi.y, hi.z, skip, ref)
   const float ix = T.inv.x, iy = T.inv.y, iz = T.inv.z;
   const float ax = (q0.x - o.x) * ix, bx = (q0.w - o.x) * ix;
@@ -375,7 +388,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   // block runs only when a lane of the wave sits at its kind (a wave-uniform branch: scene 7 +3 %)
   bool hit = false;
   float t = 0.0f;
-  if (__ballot(kind == RT_KIND_SPHERE) != 0ull) {
+  if (run_sph) {
     const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
     const float b = dot(oc, d);
     const float c = dot(oc, oc) - q0.w;
@@ -393,7 +406,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     hit = kind == RT_KIND_SPHERE && !(disc < 0) && (take1 || take2);
     t = take1 ? r1 : r2;
   }
-  if ((F & RT_FEAT_QUAD) && __ballot(kind == RT_KIND_QUAD) != 0ull) {
+  if ((F & RT_FEAT_QUAD) && run_quad) {
     const f3 nq = mk(q0.x, q0.y, q0.z);
     const float denom = dot(nq, d);
     const float tt = (q0.w - dot(nq, o)) / denom;
@@ -414,6 +427,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     T.h.xform = T.frame;
     T.found = true;
   }
+  if (waits) return false;  // (stays on its entry: no hit, no extra boxes)
   uint32_t next = skip ? __builtin_bit_cast(uint32_t, q1.z) : T.p + 1;
   // up to `extra` further actions in the same step while the next entry is a box (two thirds of the
   // scan): their LDS reads and slab tests overlap the sphere / quad chains above (T.tmax as those
@@ -627,7 +641,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             bool fin = false;
             GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
+            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1, V.wait_min);
             GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
             gs_c = GS_NOW();
             if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);

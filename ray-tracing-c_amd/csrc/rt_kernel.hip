@@ -552,7 +552,7 @@ struct Config {
   int chain_pad_k = 8;
   float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
-  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
+  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3, gen_wait = 1;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
@@ -632,6 +632,8 @@ struct Config {
     c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
     c.gen_flat = env_int("RT_GEN_FLAT", c.gen_flat);
     if (c.gen_flat < 1) c.gen_flat = 1;
+    c.gen_wait = env_int("RT_GEN_WAIT", c.gen_wait);
+    c.gen_wait = c.gen_wait < 1 ? 1 : (c.gen_wait > 64 ? 64 : c.gen_wait);
 #endif
     return c;
   }
@@ -1446,6 +1448,7 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.steps = d->cfg.gen_steps;
   V.rare_min = d->cfg.gen_rare;
   V.flat = d->cfg.gen_flat;
+  V.wait_min = d->cfg.gen_wait;
   V.n_lds = d->gen_lds;
   V.perlin_lds = d->gen_perlin_lds;
   const size_t lds_bytes = d->gen_lds_bytes;

@@ -3,6 +3,7 @@
 #   TESTS=1      pytest -m gpu (all parity tests)
 #   BENCH=1      the default bench line (N=1, parity-checked)
 #   AB="ab/r03.so;tree;diag:RT_LEAF_MIN=16"  same-box A/B of library builds / diag settings, ROUNDS rounds
+#   AB7="..."    the same on config 5 (scene 7)
 #                (entries: a path, "tree" = the product library, "diag:<VAR=V ...>" = the diagnostic build
 #                under those variables); BENCH_ARGS for other configurations
 #   S7=1         the config-5 bench line (scene 7)
@@ -20,8 +21,8 @@ step() {
 summ() { grep '^{' "$1" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('value', d['value'], 'kernel_ms', r['kernel_ms_avg'], 'parity', (d.get('parity') or {}).get('pixel_identical_to_reference'), 'build', r['build_id'])"; }
 [ "${TESTS:-0}" = 1 ] && step pytest 900 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
 [ "${BENCH:-0}" = 1 ] && step bench 300 python bench.py --no-cpu-baseline
-if [ -n "${AB:-}" ]; then
-  IFS=';' read -ra E <<< "$AB"
+ab() {  # ab "<entries>" "<bench args>"
+  IFS=';' read -ra E <<< "$1"
   for r in $(seq 1 ${ROUNDS:-2}); do
     for e in "${E[@]}"; do
       vars=""; lib=""
@@ -31,14 +32,17 @@ if [ -n "${AB:-}" ]; then
         *) lib="$e" ;;
       esac
       if [ -n "$lib" ]; then export RTC_LIB=$GRAFT_REPO_ROOT/$lib; else unset RTC_LIB; fi
-      env $vars timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity ${BENCH_ARGS:-} > gpurun_out/${TAG}_ab.log 2>&1
+      env $vars timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity $2 > gpurun_out/${TAG}_ab.log 2>&1
       rc=$?
       echo "== [$e] round $r rc=$rc $(summ gpurun_out/${TAG}_ab.log 2>&1)"
       [ $rc -ne 0 ] && { tail -5 gpurun_out/${TAG}_ab.log; exit $rc; }
     done
   done
   unset RTC_LIB
-fi
+}
+[ -n "${AB:-}" ] && ab "$AB" "${BENCH_ARGS:-}"
+# AB7: the same for config 5 (scene 7, 1000x1000x1000 spp, one frame)
+[ -n "${AB7:-}" ] && ab "$AB7" "--scene 7 --width 1000 --steps 1 --warmup 1"
 [ "${S7:-0}" = 1 ] && step s7_bench 300 python bench.py --no-cpu-baseline --scene 7 --width 1000 --steps 1 --warmup 1
 [ "${SHARD:-0}" = 1 ] && step shard 400 python -u scripts/shard_probe.py ${WORLDS:-2,4,8} all 1000
 # SHARD_ENVS="RT_CHAIN_PAD=1.2;...": the shard probe on the diagnostic build under each setting
