@@ -96,7 +96,8 @@ double rt_scene_last_launch_ms(rt_device_scene *dscene);
  * item in item order: pixel, segment, K, whole-wave (1) / lane (0), start, end (wall_clock64 ticks,
  * 100 MHz, low 32 bits), records written (samples for segment 0 / unsplit), flags (bit 0 coupled,
  * bit 1 ended), link segment, link record, segment length (draws), the pixel's pre-pass draws, the
- * pixel's pre-pass cost (traversal steps), 3 reserved (0).
+ * pixel's pre-pass cost (traversal steps), the tick at which a helper wave took the item over (tail
+ * migration; 0: never migrated), 2 reserved (0).
  * Returns the number of items (at most max_rows rows are written), -1 on error. */
 int64_t rt_scene_chain_diag(rt_device_scene *dscene, uint32_t *rows, int64_t max_rows);
 

@@ -141,7 +141,7 @@ struct Book1View {
   uint64_t *spill;           // [chunk][global lane]: a deep path's older 4-id chunks (Record)
   int32_t spill_lanes;
   int32_t n_bf_leaves;       // whole-wave pixels: leaves for bf_candidate; 0: off (coop_trace9 instead)
-  uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end}, wall_clock64 low bits
+  uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end, migrated}, wall_clock64 low bits
   // chain render (kMode 2)
   const ChainPx *ch_px;      // per pixel
   const uint2 *ch_items;     // {pixel, segment | kItemUnsplit}: whole-wave items first, then lanes'
@@ -150,7 +150,7 @@ struct Book1View {
   float4 *ch_col;            // records: colour, end offset (bits)
   uint32_t *ch_end;          // records: end offset (kRecFill until written)
   float4 *ch_acc0;           // per pixel: segment 0's colour sum when it coupled
-  uint32_t *seg_time;        // diagnostic (RT_PX_TIME=1): per segment {start, end} at end0 + k
+  uint32_t *seg_time;        // diagnostic (RT_PX_TIME=1): per segment {start, end, migrated} at end0 + k
   const ChainCont *ch_cont;  // continuation launch: items from here (else null)
   const uint32_t *ch_n_cont;
   // migration (MigRec): control words, queue, its capacity; mig_live: a wave with at most this many
@@ -641,8 +641,8 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
 RT_D void chain_time(const Book1View &V, int64_t pix, uint32_t seg, int end) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t now = (uint32_t)wall_clock64();
-  if (seg & kItemUnsplit) V.px_time[2 * pix + end] = now;
-  else V.seg_time[2 * (V.ch_px[pix].end0 + seg) + end] = now;
+  if (seg & kItemUnsplit) V.px_time[3 * pix + end] = now;
+  else V.seg_time[3 * (V.ch_px[pix].end0 + seg) + end] = now;
 #endif
 }
 RT_D bool chain_boundary(const Book1View &V, int64_t pix, uint32_t seg, uint32_t x, uint32_t s, f3 acc,
@@ -822,8 +822,8 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
   }
   if (kMode != 2 && lane0) write_pixel(out + pix * 3, acc, cam.spp);
   if (V.px_time && lane0 && kMode != 2) {
-    if (!res) V.px_time[2 * pix] = px_start;
-    V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+    if (!res) V.px_time[3 * pix] = px_start;
+    V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
   }
 }
 
@@ -891,6 +891,7 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
       MigRec r = *q;
       r.pix = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.pix);
       r.seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.seg);
+      if (V.px_time && l0 && kMode == 2) chain_time(V, r.pix, r.seg, 2);  // (diagnostic: when it migrated)
       int drop = 0;
 #ifdef RT_DIAG
       // (fault injection, diagnostic build only: drop the item unrun and uncounted -- chain_check_kernel
@@ -1137,7 +1138,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           if (kMode == 1)
             V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
           if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
-          if (V.px_time) V.px_time[2 * pix + 1] = (uint32_t)wall_clock64();
+          if (V.px_time) V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;
         } else {
@@ -1185,7 +1186,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         need_pixel = false;
         px_steps = 0;
-        if (V.px_time && kMode != 2) V.px_time[2 * pix] = (uint32_t)wall_clock64();
+        if (V.px_time && kMode != 2) V.px_time[3 * pix] = (uint32_t)wall_clock64();
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }
       if (kMode == 2 && chain_boundary(V, pix, seg, g.n, (uint32_t)s, acc, tc, st, out, true)) {

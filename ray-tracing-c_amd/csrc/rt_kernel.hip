@@ -667,7 +667,7 @@ struct rt_device_scene {
   int64_t deep_threads = 0;
   b1::MigRec *mig_q = nullptr;   // tail migration queue (rt_book1.h: MigRec)
   uint32_t mig_epoch = 0;        //   its entries are tagged with a per-launch epoch
-  uint32_t *px_time = nullptr;   // RT_PX_TIME diagnostic: {start, end} per work item
+  uint32_t *px_time = nullptr;   // RT_PX_TIME diagnostic: {start, end, migrated} per work item
   uint32_t *seg_time = nullptr;  //   and per chain segment
   // chain render scratch (rt_book1.h: ChainPx), sized for the whole frame at upload; records on demand
   void *ch_arena = nullptr;
@@ -975,7 +975,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->lpt_hist = (uint32_t *)(b + off[6]);
   d->draw_out = (uint32_t *)(b + off[7]);
   if (cfg.px_time) {
-    HIP_OK(hipMalloc(&d->px_time, npix * 2 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d->px_time, npix * 3 * sizeof(uint32_t)));
     V.px_time = d->px_time;
   }
 #ifdef RT_LOOP_STATS
@@ -1004,7 +1004,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
     if (cfg.px_time) {
-      HIP_OK(hipMalloc(&d->seg_time, nseg * 2 * sizeof(uint32_t)));
+      HIP_OK(hipMalloc(&d->seg_time, nseg * 3 * sizeof(uint32_t)));
       V.seg_time = d->seg_time;
     }
   }
@@ -1259,6 +1259,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   // is its longest chains)
   d->chain_occ = chain_occupancy(d, npix);
   d->chain_grid = d->chain_occ == 5 ? d->chain_grid5 : d->chain_grid3;
+  if (d->px_time) {  // (diagnostic timelines: a fresh record per launch)
+    HIP_OK(hipMemsetAsync(d->px_time, 0, (size_t)d->width * d->height * 3 * sizeof(uint32_t), st));
+    HIP_OK(hipMemsetAsync(d->seg_time, 0, (size_t)d->ch_seg_cap * 3 * sizeof(uint32_t), st));
+  }
   launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
@@ -1749,14 +1753,14 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   std::vector<uint2> items(n_items);
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg(n_seg);
-  std::vector<uint32_t> pt(2 * npix), sgt(2 * n_seg), draws(npix), costs(npix);
+  std::vector<uint32_t> pt(3 * npix), sgt(3 * n_seg), draws(npix), costs(npix);
   HIP_OK(hipMemcpy(draws.data(), d->draw_out, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(costs.data(), d->lpt_cost, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(items.data(), d->ch_items, n_items * sizeof(uint2), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(px.data(), d->ch_px, npix * sizeof(b1::ChainPx), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(seg.data(), d->ch_seg, n_seg * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(pt.data(), d->px_time, 2 * npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(sgt.data(), d->seg_time, 2 * n_seg * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(pt.data(), d->px_time, 3 * npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(sgt.data(), d->seg_time, 3 * n_seg * sizeof(uint32_t), hipMemcpyDeviceToHost));
   const uint32_t spp = (uint32_t)d->view.cam.spp;
   for (size_t k = 0; k < n_items && (int64_t)k < max_rows; k++) {
     const uint32_t p = items[k].x, sg = items[k].y;
@@ -1768,13 +1772,14 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
     r[12] = costs[p];
     r[13] = r[14] = r[15] = 0u;
     if (sg & b1::kItemUnsplit) {
-      r[1] = 0, r[2] = 1, r[4] = pt[2 * p], r[5] = pt[2 * p + 1], r[6] = spp, r[7] = 2u;
+      r[1] = 0, r[2] = 1, r[4] = pt[3 * p], r[5] = pt[3 * p + 1], r[6] = spp, r[7] = 2u, r[13] = pt[3 * p + 2];
     } else {
       const b1::ChainPx &P = px[p];
       const uint64_t w = P.end0 + sg < n_seg ? seg[P.end0 + sg] : 0ull;
       r[1] = sg, r[2] = P.K;
-      r[4] = P.end0 + sg < n_seg ? sgt[2 * (P.end0 + sg)] : 0u;
-      r[5] = P.end0 + sg < n_seg ? sgt[2 * (P.end0 + sg) + 1] : 0u;
+      r[4] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg)] : 0u;
+      r[5] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg) + 1] : 0u;
+      r[13] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg) + 2] : 0u;
       r[6] = b1::end_n(w);
       r[7] = ((w & b1::kEndEnded) && !(w & b1::kEndNoLink) ? 1u : 0u) | ((w & b1::kEndEnded) ? 2u : 0u);
       r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len;

@@ -68,9 +68,13 @@ w = np.where(r[:, 3] >= 1, 64, 1)
 inflight = [int(w[(start <= t) & (end > t)].sum()) for t in ts]
 print("  lane-equivalents in flight every 5 ms: " + " ".join(f"{t:.0f}:{v // 1000}k" for t, v in zip(ts, inflight)), flush=True)
 last = np.argsort(-end)[:16]
-print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, records, flags, link t:c, seg_len, pre-pass draws)")
+mig = np.where(r[:, 13] > 0, (r[:, 13] - t0) / 1e5, np.nan)
+print(f"  migrated to helper waves: {int(np.isfinite(mig).sum())} items, at p50/p90/max "
+      f"{np.nanpercentile(mig, [50, 90, 100]).round(1) if np.isfinite(mig).any() else '-'} ms", flush=True)
+print("  last to finish: (item, pixel, seg/K, wave, start ms, end ms, migrated ms, records, flags, link t:c, seg_len, pre-pass draws)")
 for q in last:
-    print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {r[q, 6]:5d} {r[q, 7]} {r[q, 8]}:{r[q, 9]} {r[q, 10]} {r[q, 11]}")
+    print(f"    {q:7d} {r[q, 0]:7d} {r[q, 1]}/{r[q, 2]} {r[q, 3]} {start[q]:7.1f} {end[q]:7.1f} {mig[q]:7.1f} {r[q, 6]:5d} {r[q, 7]} "
+          f"{r[q, 8]}:{r[q, 9]} {r[q, 10]} {r[q, 11]}")
 if os.environ.get("CHAIN_ROWS"):  # the item rows for offline analysis (uint32, compressed)
     np.savez_compressed(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", f"chain_rows_{world}_{rank}{os.environ.get('CHAIN_TAG', '')}.npz"),
                         rows=rows)
