@@ -177,7 +177,6 @@ def main():
     W, H, spp = sc.width, sc.height, sc.spp
     row0, stride, n_rows = rtc.rows_of(H, rank, world)
     ds = rtc.DeviceScene(sc, local)
-    kernel_name = ds.kernel_name
     buf = torch.zeros((max(n_rows, 1), W, 3), dtype=torch.uint8, device=f"cuda:{local}")
     stream = torch.cuda.current_stream(local)
 
@@ -192,6 +191,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    kernel_name = ds.kernel_name  # (after a launch: the instantiation this rank's share actually runs)
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]

@@ -240,6 +240,20 @@ __global__ void lpt_hist_kernel(const uint32_t *cost, int n, uint32_t *hist, uns
   }
 }
 
+// The pre-pass cost as the planner uses it (RT_COST_SMOOTH = h > 0, diagnostic build): the larger of a
+// pixel's own 16-spp cost and the mean over its row neighbours +-h -- a pixel whose few samples were
+// cheap, among expensive neighbours, is planned (split, started) like its neighbours.
+__global__ void cost_smooth_kernel(uint32_t *cost, const uint32_t *own, int n, int width, int h) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+    const int row = p / width, x = p - row * width;
+    const int x0 = max(0, x - h), x1 = min(width - 1, x + h);
+    uint64_t sum = 0;
+    for (int q = x0; q <= x1; q++) sum += own[row * width + q];
+    const uint32_t avg = (uint32_t)(sum / (uint64_t)(x1 - x0 + 1));
+    cost[p] = max(own[p], avg);
+  }
+}
+
 // LPT scratch (u32): 256 bucket counts, 256 running offsets, then from u32 544 the 256 per-bucket
 // step sums (u64).
 constexpr size_t kLptHistBytes = 8192;
@@ -562,6 +576,7 @@ struct Config {
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
+  int cost_smooth = 0;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -588,6 +603,8 @@ struct Config {
     c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
+    c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
+    c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
     c.general = env_flag("RT_GENERAL", true);
@@ -663,6 +680,7 @@ struct rt_device_scene {
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
   uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
+  uint32_t *cost_own = nullptr;  // RT_COST_SMOOTH: the pre-pass's own costs (W*H), lpt_cost the smoothed ones
   DeepRec *deep_rec = nullptr;   // max_depth > kMaxDepth: path records (rt_render_deep_kernel)
   int64_t deep_threads = 0;
   b1::MigRec *mig_q = nullptr;   // tail migration queue (rt_book1.h: MigRec)
@@ -974,6 +992,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->lpt_order = (int32_t *)(b + off[5]);
   d->lpt_hist = (uint32_t *)(b + off[6]);
   d->draw_out = (uint32_t *)(b + off[7]);
+  if (cfg.cost_smooth > 0) HIP_OK(hipMalloc(&d->cost_own, npix * sizeof(uint32_t)));
   if (cfg.px_time) {
     HIP_OK(hipMalloc(&d->px_time, npix * 3 * sizeof(uint32_t)));
     V.px_time = d->px_time;
@@ -1183,6 +1202,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->gen_xrec) (void)hipFree(d->gen_xrec);
   if (d->px_time) (void)hipFree(d->px_time);
+  if (d->cost_own) (void)hipFree(d->cost_own);
   if (d->seg_time) (void)hipFree(d->seg_time);
   if (d->mig_q) (void)hipFree(d->mig_q);
   if (d->deep_rec) (void)hipFree(d->deep_rec);
@@ -1200,7 +1220,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
 static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st) {
   (void)hipMemsetAsync(P.work_counter, 0, kCounterBytes, st);  // (the previous launch left it past its items)
   P.S.cam.spp = d->cfg.lpt_spp;
-  P.cost_out = d->lpt_cost;
+  P.cost_out = d->cost_own ? d->cost_own : d->lpt_cost;
   P.draw_out = d->draw_out;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.n_coop = nullptr;
@@ -1269,6 +1289,9 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   HIP_OK(hipMemsetAsync(d->ch_cnt, 0, kCnWords * sizeof(uint32_t), st));
   unsigned long long *sums = (unsigned long long *)(d->lpt_hist + 512 + 32);
   const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+  if (d->cost_own)
+    hipLaunchKernelGGL(cost_smooth_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, (const uint32_t *)d->cost_own, n,
+                       V.S.cam.width, cfg.cost_smooth);
   hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
   ChainModel m;
   m.ratio = (float)V.S.cam.spp / (float)cfg.lpt_spp;
@@ -1789,8 +1812,9 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   return (int64_t)k;
 }
 
-// Name of the frame kernel rt_render_rows_async launches for this scene over the whole image (as
-// rocprofv3 reports it).
+// Name of the frame kernel rt_render_rows_async launched last on this scene -- or, before any launch,
+// the one it would launch over the whole image -- as rocprofv3 reports it (the chain kernel's
+// occupancy depends on the launch's pixel count: a rank's share can get the 3-wave instantiation).
 extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   static thread_local char buf[160];
   if (!d) return "";
@@ -1809,7 +1833,7 @@ extern "C" const char *rt_scene_kernel(const rt_device_scene *d) {
   const int mode = pick_mode(d, npix);
   const char *lds = d->b1_lds_bytes ? "true" : "false";
   if (mode == kModeChain)  // (every template argument, as rocprofv3 demangles the name: kLds, kOcc)
-    snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %d>", lds, chain_occupancy(d, npix));
+    snprintf(buf, sizeof buf, "rt_book1_chain_kernel<%s, %d>", lds, d->launched ? d->chain_occ : chain_occupancy(d, npix));
   else
     snprintf(buf, sizeof buf, "rt_book1_kernel<%s>", lds);
   return buf;
