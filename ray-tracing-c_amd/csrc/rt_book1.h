@@ -134,6 +134,8 @@ struct Book1View {
   int32_t leaf_min;          // trav_step_v9: a leaf's sphere test waits until this many stepping lanes are at leaves
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
+  int32_t pre_split;         // cost pre-pass: > 1: a work item is one of a pixel's pre_split samples, each
+                             // from its own stream offset (q * kPreStride), cost and draws summed per pixel
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
@@ -950,6 +952,9 @@ __device__ __attribute__((noinline)) void coop_items(const Book1View &V, const f
 }
 
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
+// pre-pass samples of one pixel start this far apart in its stream (any offsets give samples of the
+// same distribution; these never overlap within the ~10^2 draws of a sample)
+constexpr uint32_t kPreStride = 1u << 20;
 // traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
 // 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
 // schedule never changes a lane)
@@ -1022,6 +1027,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const int64_t work_offset = kMode == 2 && V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   const int64_t total_own = cont ? (int64_t)*V.ch_n_cont
                             : kMode == 2 ? (int64_t)*V.ch_n_items - work_offset
+                            : kMode == 1 && V.pre_split > 1 ? total * V.pre_split
                                          : total - work_offset;
 
   for (;;) {
@@ -1135,9 +1141,13 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          if (kMode == 1)
+          if (kMode == 1 && V.pre_split > 1) {  // one of the pixel's pre-pass samples (st: its start offset)
+            atomicAdd(&V.cost_out[pix], px_steps);
+            atomicAdd(&V.draw_out[pix], g.n - st);
+          } else if (kMode == 1) {
             V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
-          if (kMode == 1) V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
+            V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
+          }
           if (V.px_time) V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;
@@ -1172,6 +1182,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           const uint2 it = V.ch_items[item + work_offset];
           pix = (int32_t)it.x;
           seg = it.y;
+        } else if (kMode == 1 && V.pre_split > 1) {
+          pix = (int32_t)(item / V.pre_split);  // (item: one sample of a pixel, below)
         } else {
           pix = (int32_t)item;  // (lane launches: low spp / small images, in pixel order)
         }
@@ -1179,7 +1191,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
           g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
         }
-        if (kMode == 2 && cont) {
+        if (kMode == 1 && V.pre_split > 1) {  // the pixel's pre-pass sample q, from stream offset q * kPreStride
+          g.skip((uint32_t)(item - (int64_t)pix * V.pre_split) * kPreStride);
+          st = g.n;
+        } else if (kMode == 2 && cont) {
           g.skip(st);
         } else if (kMode == 2 && !(seg & kItemUnsplit)) {
           chain_start(V, (uint32_t)pix, seg, g, tc, st);

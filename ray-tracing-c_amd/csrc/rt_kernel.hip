@@ -577,6 +577,7 @@ struct Config {
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int cost_smooth = 0;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
+  bool pre_split = false;  // cost pre-pass: one work item per sample (rt_book1.h: Book1View.pre_split)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -604,6 +605,7 @@ struct Config {
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
+    c.pre_split = env_flag("RT_PRE_SPLIT", c.pre_split);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -1217,11 +1219,18 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
 }
 
 // ------------------------------------------------------------------------------ launches
-static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st) {
+static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st, int64_t npix) {
   (void)hipMemsetAsync(P.work_counter, 0, kCounterBytes, st);  // (the previous launch left it past its items)
   P.S.cam.spp = d->cfg.lpt_spp;
   P.cost_out = d->cost_own ? d->cost_own : d->lpt_cost;
   P.draw_out = d->draw_out;
+  P.pre_split = 0;
+  if (d->cfg.pre_split && d->cfg.lpt_spp > 1) {  // one work item per pre-pass sample: sums per pixel
+    P.pre_split = d->cfg.lpt_spp;
+    P.S.cam.spp = 1;
+    (void)hipMemsetAsync(P.cost_out, 0, (size_t)npix * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(P.draw_out, 0, (size_t)npix * sizeof(uint32_t), st);
+  }
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.n_coop = nullptr;
   // at the chain kernel's occupancy, on its grid
@@ -1283,7 +1292,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
     HIP_OK(hipMemsetAsync(d->px_time, 0, (size_t)d->width * d->height * 3 * sizeof(uint32_t), st));
     HIP_OK(hipMemsetAsync(d->seg_time, 0, (size_t)d->ch_seg_cap * 3 * sizeof(uint32_t), st));
   }
-  launch_cost_pass(d, V, d_out, st);
+  launch_cost_pass(d, V, d_out, st, npix);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
   HIP_OK(hipMemsetAsync(d->ch_cnt, 0, kCnWords * sizeof(uint32_t), st));
