@@ -1508,10 +1508,10 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
 static int pick_mode(const rt_device_scene *d, int64_t npix) {
   const Config &cfg = d->cfg;
   const int spp = d->view.cam.spp;
-  // (the pre-pass at most at the frame's spp; RT_LPT_SPP = spp is the diagnostic "exact stream lengths"
-  // plan of scripts/gpu_tail_data.sh)
-  const bool chain_ok = cfg.lpt && spp >= 64 && cfg.lpt_spp <= spp && spp >= 2 * cfg.chain_min_seg &&
-                        npix >= 4096 && d->view.cam.max_depth >= 1;
+  // (a pre-pass of at most a quarter of the frame's spp -- or exactly its spp: the diagnostic "exact
+  // stream lengths" plan of scripts/gpu_r04.sh, RT_LPT_SPP = spp)
+  const bool chain_ok = cfg.lpt && (spp >= 4 * cfg.lpt_spp || (cfg.lpt_spp == spp && spp >= 64)) &&
+                        spp >= 2 * cfg.chain_min_seg && npix >= 4096 && d->view.cam.max_depth >= 1;
   if (cfg.mode == kModeChain) return chain_ok ? kModeChain : kModeLane;
   if (cfg.mode == kModeLane) return kModeLane;
   // auto: the chain render whenever it applies (measured ahead of the lane kernel at every N, from
