@@ -131,11 +131,8 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
-  int32_t leaf_min;          // trav_step_v9: a leaf's sphere test waits until this many stepping lanes are at leaves
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
-  int32_t pre_split;         // cost pre-pass: > 1: a work item is one of a pixel's pre_split samples, each
-                             // from its own stream offset (q * kPreStride), cost and draws summed per pixel
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
@@ -299,13 +296,10 @@ RT_D float4 it_q1(const float4 *items, int na, uint32_t p) { return items[(uint3
 
 // L.cur, na16 and n16 are byte offsets (item index x 16): na16 = 16 V.n_items9_alloc, n16 = 16 V.n_items9
 // (hoisted by the caller, in VGPRs) -- the step then needs no index scaling.
-// Leaves wait for company: a lane at a leaf runs its sphere test only once at least leaf_min of the
-// stepping lanes sit at leaves (or no lane sits at a node); until then it stays on its item while
-// the node lanes go on.  Leaves are ~6 % of the scan's items (7.2 sphere tests per 111 boxes a ray,
-// SURVEY §8d), so in an if-if step some lane of the wave is at a leaf nearly every time and the
-// sphere block ran for one or two lanes; a lane's own sequence of items is unchanged (exact).
-// The caller calls this with exec = the stepping lanes (the ballots count those).
-RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L, float tmin, int leaf_min = 1) {
+// (Leaves waiting for company -- a lane at a leaf running its sphere test only once 8 / 16 / 32 lanes
+// sit at leaves, the node lanes going on meanwhile -- measured 1 / 6 / 24 % slower, r04: the waiting
+// lanes' latency costs more than the sphere block saves.)
+RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L, float tmin) {
   const uint32_t p = L.cur;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const char *base = (const char *)items;
@@ -320,15 +314,8 @@ RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L
   // (branches, not both tests straight-line for every lane: a wave's lanes are mostly at one kind --
   // the straight-line step measured 1.3x slower)
   uint32_t next = p + 16u;
-  const bool leaf = (w & kLeaf9) != 0u;
-  bool do_leaf = true;
-  if (leaf_min > 1) {  // (wave-uniform)
-    const uint64_t lm = __ballot(leaf), all = __ballot(true);
-    do_leaf = lm == all || (int)__popcll(lm) >= leaf_min;
-  }
-  if (leaf) {
-    if (do_leaf) sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
-    else next = p;  // waits at its leaf
+  if (w & kLeaf9) {
+    sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
   } else {
     if (!aabb_packed(q0, q1, L, tmin)) next = p + (__float_as_uint(q1.z) << 4);
   }
@@ -952,9 +939,6 @@ __device__ __attribute__((noinline)) void coop_items(const Book1View &V, const f
 }
 
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
-// pre-pass samples of one pixel start this far apart in its stream (any offsets give samples of the
-// same distribution; these never overlap within the ~10^2 draws of a sample)
-constexpr uint32_t kPreStride = 1u << 20;
 // traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
 // 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
 // schedule never changes a lane)
@@ -1027,7 +1011,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   const int64_t work_offset = kMode == 2 && V.n_coop != nullptr ? (int64_t)*V.n_coop : 0;
   const int64_t total_own = cont ? (int64_t)*V.ch_n_cont
                             : kMode == 2 ? (int64_t)*V.ch_n_items - work_offset
-                            : kMode == 1 && V.pre_split > 1 ? total * V.pre_split
                                          : total - work_offset;
 
   for (;;) {
@@ -1062,9 +1045,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
 #pragma unroll
           for (int u = 0; u < kSteps; u++)
             if (mode == kTrav) {
-              const uint32_t at = L.cur;
-              if (trav_step_v9(items9, na, n9, L, tmin, V.leaf_min)) mode = kWait;
-              if (kMode == 1) px_steps += L.cur != at;  // work-item cost (the LPT pre-pass): items visited
+              if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
+              if (trav_step_v9(items9, na, n9, L, tmin)) mode = kWait;
             }
         }
         const uint64_t t2 = __ballot(mode == kTrav), w2 = __ballot(mode == kWait);
@@ -1141,10 +1123,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const bool cut = kMode == 1 && px_steps >= V.cost_budget && s < spp;
         if (kMode != 2 && (s == spp || cut)) {  // quantize (src/raytracing.c:127-131)
           if (kMode != 1) write_pixel(out + pix * 3, acc, spp);  // (the pre-pass's image is not used)
-          if (kMode == 1 && V.pre_split > 1) {  // one of the pixel's pre-pass samples (st: its start offset)
-            atomicAdd(&V.cost_out[pix], px_steps);
-            atomicAdd(&V.draw_out[pix], g.n - st);
-          } else if (kMode == 1) {
+          if (kMode == 1) {
             V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
             V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
           }
@@ -1182,8 +1161,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           const uint2 it = V.ch_items[item + work_offset];
           pix = (int32_t)it.x;
           seg = it.y;
-        } else if (kMode == 1 && V.pre_split > 1) {
-          pix = (int32_t)(item / V.pre_split);  // (item: one sample of a pixel, below)
         } else {
           pix = (int32_t)item;  // (lane launches: low spp / small images, in pixel order)
         }
@@ -1191,10 +1168,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
           g.seed((uint64_t)(17 + j), (uint64_t)(23 + i));  // src/raytracing.c:94
         }
-        if (kMode == 1 && V.pre_split > 1) {  // the pixel's pre-pass sample q, from stream offset q * kPreStride
-          g.skip((uint32_t)(item - (int64_t)pix * V.pre_split) * kPreStride);
-          st = g.n;
-        } else if (kMode == 2 && cont) {
+        if (kMode == 2 && cont) {
           g.skip(st);
         } else if (kMode == 2 && !(seg & kItemUnsplit)) {
           chain_start(V, (uint32_t)pix, seg, g, tc, st);

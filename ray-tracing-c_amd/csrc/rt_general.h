@@ -24,7 +24,6 @@ struct GeneralView {
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
   int32_t rare_min;          // kBatch: run rare scan actions once this many lanes wait at one (RT_GEN_RARE)
-  int32_t wait_min;          // kBatch: a lane at a sphere / quad waits until this many stepping lanes are at one (1: never)
   int32_t flat;              // kBatch: common entries as one straight-line block (pre_common) plus up to
                              // flat - 1 box entries in the same step (RT_GEN_FLAT, >= 1)
   unsigned long long *stats;  // diagnostic builds (-DRT_GEN_STATS): kGs* counters, summed over waves
@@ -86,54 +85,77 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
 // (DESIGN.md §4.3); with 8 weights and 2 albedos in registers nearly no path touches memory, where
 // every record store used to leave L2 for HBM at >= 32 B.  Only static register indices (unrolled
 // shifts): a dynamically indexed private array would live in scratch.
+#ifndef RT_GEN_WREG
+#define RT_GEN_WREG 8  // pdf weights in registers
+#endif
+#ifndef RT_GEN_XREG
+#define RT_GEN_XREG 2  // explicit albedos in registers
+#endif
+constexpr int kWReg = RT_GEN_WREG, kXReg = RT_GEN_XREG;
 template <int kN>
 struct RegStack {
-  float v[kN];
+  float v[kN > 0 ? kN : 1];
   int n;  // entries pushed and not popped (the newest min(n, kN) in v, newest first)
 };
 template <int kN>
-RT_D void rs_clear(RegStack<kN> &S) { S.n = 0; }
-template <int kN>
 RT_D void rs_push(RegStack<kN> &S, float x, float *spill) {
-  if (S.n >= kN) spill[S.n - kN] = S.v[kN - 1];
+  if constexpr (kN == 0) {
+    spill[S.n] = x;
+  } else {
+    if (S.n >= kN) spill[S.n - kN] = S.v[kN - 1];
 #pragma unroll
-  for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
-  S.v[0] = x;
+    for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
+    S.v[0] = x;
+  }
   S.n++;
 }
 template <int kN>
 RT_D float rs_pop(RegStack<kN> &S, const float *spill) {
-  const float x = S.v[0];
-#pragma unroll
-  for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
   S.n--;
-  if (S.n >= kN) S.v[kN - 1] = spill[S.n - kN];
-  return x;
+  if constexpr (kN == 0) {
+    return spill[S.n];
+  } else {
+    const float x = S.v[0];
+#pragma unroll
+    for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
+    if (S.n >= kN) S.v[kN - 1] = spill[S.n - kN];
+    return x;
+  }
 }
-struct XStack {  // explicit albedos: kXReg in registers
-  static constexpr int kN = 2;
-  f3 v[kN];
+template <int kN>
+struct XStack {  // explicit albedos
+  f3 v[kN > 0 ? kN : 1];
   int n;
 };
-RT_D void xs_push(XStack &S, f3 x, float4 *spill) {
-  if (S.n >= XStack::kN) spill[S.n - XStack::kN] = make_float4(S.v[XStack::kN - 1].x, S.v[XStack::kN - 1].y, S.v[XStack::kN - 1].z, 0.0f);
+template <int kN>
+RT_D void xs_push(XStack<kN> &S, f3 x, float4 *spill) {
+  if constexpr (kN == 0) {
+    spill[S.n] = make_float4(x.x, x.y, x.z, 0.0f);
+  } else {
+    if (S.n >= kN) spill[S.n - kN] = make_float4(S.v[kN - 1].x, S.v[kN - 1].y, S.v[kN - 1].z, 0.0f);
 #pragma unroll
-  for (int k = XStack::kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
-  S.v[0] = x;
+    for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
+    S.v[0] = x;
+  }
   S.n++;
 }
-RT_D f3 xs_pop(XStack &S, const float4 *spill) {
-  const f3 x = S.v[0];
-#pragma unroll
-  for (int k = 0; k < XStack::kN - 1; k++) S.v[k] = S.v[k + 1];
+template <int kN>
+RT_D f3 xs_pop(XStack<kN> &S, const float4 *spill) {
   S.n--;
-  if (S.n >= XStack::kN) {
-    const float4 e = spill[S.n - XStack::kN];
-    S.v[XStack::kN - 1] = mk(e.x, e.y, e.z);
+  if constexpr (kN == 0) {
+    const float4 e = spill[S.n];
+    return mk(e.x, e.y, e.z);
+  } else {
+    const f3 x = S.v[0];
+#pragma unroll
+    for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
+    if (S.n >= kN) {
+      const float4 e = spill[S.n - kN];
+      S.v[kN - 1] = mk(e.x, e.y, e.z);
+    }
+    return x;
   }
-  return x;
 }
-constexpr int kWReg = 8;  // pdf weights in registers
 
 // -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
 enum {
@@ -358,24 +380,14 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
 // only the quad's in-plane test (its record: measured no faster when loaded up front) and the
 // sphere's out-of-range fallback branch.
 // Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
-// wait_min > 1: a lane at a sphere (a quad) waits on its entry while lanes sit at boxes, until at least
-// wait_min of the stepping lanes are at spheres (quads) -- the block then runs for more lanes at once
-// (Book-1's leaf wait, rt_book1.h trav_step_v9); a lane's own entry sequence is unchanged.  The caller
-// calls this with exec = the stepping lanes (the ballots count those).
+// (Sphere / quad lanes waiting for company while lanes sit at boxes, as rt_book1.h's measured leaf
+// wait: 8 / 16 lanes 14 / 58 % slower on config 5, r04.)
 template <int F>
 RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin, float4 q0, float4 q1,
-                     int extra = 0, int wait_min = 1) {
+                     int extra = 0) {
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
   const int kind = rt_ref_kind(ref);
   const f3 o = T.o, d = T.d;
-  const uint64_t m_sph = __ballot(kind == RT_KIND_SPHERE), m_quad = (F & RT_FEAT_QUAD) ? __ballot(kind == RT_KIND_QUAD) : 0ull;
-  bool run_sph = m_sph != 0ull, run_quad = m_quad != 0ull;
-  if (wait_min > 1) {  // (wave-uniform)
-    const bool boxes = __ballot(kind == RT_KIND_BVH) != 0ull;
-    run_sph = run_sph && (!boxes || (int)__popcll(m_sph) >= wait_min);
-    run_quad = run_quad && (!boxes || (int)__popcll(m_quad) >= wait_min);
-  }
-  const bool waits = (kind == RT_KIND_SPHERE && !run_sph) || (kind == RT_KIND_QUAD && !run_quad);
   // box: q0 = (lo.x, lo.y, lo.z, hi.x), q1 = (hi.y, hi.z, skip, ref)
   const float ix = T.inv.x, iy = T.inv.y, iz = T.inv.z;
   const float ax = (q0.x - o.x) * ix, bx = (q0.w - o.x) * ix;
@@ -388,7 +400,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   // block runs only when a lane of the wave sits at its kind (a wave-uniform branch: scene 7 +3 %)
   bool hit = false;
   float t = 0.0f;
-  if (run_sph) {
+  if (__ballot(kind == RT_KIND_SPHERE) != 0ull) {
     const f3 oc = sub(o, mk(q0.x, q0.y, q0.z));
     const float b = dot(oc, d);
     const float c = dot(oc, oc) - q0.w;
@@ -406,7 +418,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     hit = kind == RT_KIND_SPHERE && !(disc < 0) && (take1 || take2);
     t = take1 ? r1 : r2;
   }
-  if ((F & RT_FEAT_QUAD) && run_quad) {
+  if ((F & RT_FEAT_QUAD) && __ballot(kind == RT_KIND_QUAD) != 0ull) {
     const f3 nq = mk(q0.x, q0.y, q0.z);
     const float denom = dot(nq, d);
     const float tt = (q0.w - dot(nq, o)) / denom;
@@ -427,7 +439,6 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     T.h.xform = T.frame;
     T.found = true;
   }
-  if (waits) return false;  // (stays on its entry: no hit, no extra boxes)
   uint32_t next = skip ? __builtin_bit_cast(uint32_t, q1.z) : T.p + 1;
   // up to `extra` further actions in the same step while the next entry is a box (two thirds of the
   // scan): their LDS reads and slab tests overlap the sphere / quad chains above (T.tmax as those
@@ -515,11 +526,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   // kMaxDepth global slots)
   const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
   RegStack<kWReg> wst;
-  XStack xst;
+  XStack<kXReg> xst;
 #pragma unroll
-  for (int k = 0; k < kWReg; k++) wst.v[k] = 1.0f;
+  for (int k = 0; k < (kWReg > 0 ? kWReg : 1); k++) wst.v[k] = 1.0f;
 #pragma unroll
-  for (int k = 0; k < XStack::kN; k++) xst.v[k] = mk(0.0f, 0.0f, 0.0f);
+  for (int k = 0; k < (kXReg > 0 ? kXReg : 1); k++) xst.v[k] = mk(0.0f, 0.0f, 0.0f);
   wst.n = 0, xst.n = 0;
   int n = 0, depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
@@ -641,7 +652,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             bool fin = false;
             GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1, V.wait_min);
+            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
             GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
             gs_c = GS_NOW();
             if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);

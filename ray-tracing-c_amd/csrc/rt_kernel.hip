@@ -557,16 +557,16 @@ enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
   bool lpt = true, bf = true, px_time = false, debug = false;
-  int lpt_spp = 16, shade_batch = 48, leaf_min = 1;
+  int lpt_spp = 16, shade_batch = 48;
   int mode = kModeAuto;
   float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
-  float chain_pad = 1.0f;  // padded plan (chain_plan_kernel): off at 1
+  float chain_pad = 1.2f;  // padded plan (chain_plan_kernel; 1: off) for pixels of >= chain_pad_k segments
   int chain_pad_k = 8;
   float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
   size_t chain_mb = 24576;  // record arena budget (MiB; the planner keeps pixels whole beyond it)
-  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3, gen_wait = 1;
+  int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
@@ -576,8 +576,7 @@ struct Config {
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
-  int cost_smooth = 0;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
-  bool pre_split = false;  // cost pre-pass: one work item per sample (rt_book1.h: Book1View.pre_split)
+  int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -605,7 +604,6 @@ struct Config {
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
-    c.pre_split = env_flag("RT_PRE_SPLIT", c.pre_split);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -615,8 +613,6 @@ struct Config {
     c.bf = env_flag("RT_BF", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
-    c.leaf_min = env_int("RT_LEAF_MIN", c.leaf_min);
-    c.leaf_min = c.leaf_min < 1 ? 1 : (c.leaf_min > 64 ? 64 : c.leaf_min);
     c.shade_batch = env_int("RT_SHADE_BATCH", c.shade_batch);
     c.shade_batch = c.shade_batch < 1 ? 1 : (c.shade_batch > 64 ? 64 : c.shade_batch);  // >= 1: progress
     if (const char *m = getenv("RT_MODE")) {
@@ -651,8 +647,6 @@ struct Config {
     c.gen_rare = env_int("RT_GEN_RARE", c.gen_rare);
     c.gen_flat = env_int("RT_GEN_FLAT", c.gen_flat);
     if (c.gen_flat < 1) c.gen_flat = 1;
-    c.gen_wait = env_int("RT_GEN_WAIT", c.gen_wait);
-    c.gen_wait = c.gen_wait < 1 ? 1 : (c.gen_wait > 64 ? 64 : c.gen_wait);
 #endif
     return c;
   }
@@ -988,7 +982,6 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.spill = (uint64_t *)(b + off[3]);
   V.spill_lanes = spill_lanes;
   V.shade_batch = cfg.shade_batch;
-  V.leaf_min = cfg.leaf_min;
   V.n_bf_leaves = H.n_bf;
   d->lpt_cost = (uint32_t *)(b + off[4]);
   d->lpt_order = (int32_t *)(b + off[5]);
@@ -1219,18 +1212,11 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
 }
 
 // ------------------------------------------------------------------------------ launches
-static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st, int64_t npix) {
+static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st) {
   (void)hipMemsetAsync(P.work_counter, 0, kCounterBytes, st);  // (the previous launch left it past its items)
   P.S.cam.spp = d->cfg.lpt_spp;
   P.cost_out = d->cost_own ? d->cost_own : d->lpt_cost;
   P.draw_out = d->draw_out;
-  P.pre_split = 0;
-  if (d->cfg.pre_split && d->cfg.lpt_spp > 1) {  // one work item per pre-pass sample: sums per pixel
-    P.pre_split = d->cfg.lpt_spp;
-    P.S.cam.spp = 1;
-    (void)hipMemsetAsync(P.cost_out, 0, (size_t)npix * sizeof(uint32_t), st);
-    (void)hipMemsetAsync(P.draw_out, 0, (size_t)npix * sizeof(uint32_t), st);
-  }
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.n_coop = nullptr;
   // at the chain kernel's occupancy, on its grid
@@ -1292,7 +1278,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
     HIP_OK(hipMemsetAsync(d->px_time, 0, (size_t)d->width * d->height * 3 * sizeof(uint32_t), st));
     HIP_OK(hipMemsetAsync(d->seg_time, 0, (size_t)d->ch_seg_cap * 3 * sizeof(uint32_t), st));
   }
-  launch_cost_pass(d, V, d_out, st, npix);
+  launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
   HIP_OK(hipMemsetAsync(d->ch_cnt, 0, kCnWords * sizeof(uint32_t), st));
@@ -1484,7 +1470,6 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
   V.steps = d->cfg.gen_steps;
   V.rare_min = d->cfg.gen_rare;
   V.flat = d->cfg.gen_flat;
-  V.wait_min = d->cfg.gen_wait;
   V.n_lds = d->gen_lds;
   V.perlin_lds = d->gen_perlin_lds;
   const size_t lds_bytes = d->gen_lds_bytes;
