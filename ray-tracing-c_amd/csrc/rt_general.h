@@ -82,14 +82,14 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
 // registers (the fold visits records newest first, i.e. in reverse push order): a push into a full
 // register part moves its oldest entry to the thread's global slots, a pop refills the register part
 // from there.  Scene 7 averages 4.37 records per sample, 3.9 of them weighted and 0.65 explicit
-// (DESIGN.md §4.3); with 8 weights and 2 albedos in registers nearly no path touches memory, where
+// (DESIGN.md §4.3); with 4 weights and 1 albedo in registers most paths never touch memory, where
 // every record store used to leave L2 for HBM at >= 32 B.  Only static register indices (unrolled
 // shifts): a dynamically indexed private array would live in scratch.
 #ifndef RT_GEN_WREG
-#define RT_GEN_WREG 8  // pdf weights in registers
+#define RT_GEN_WREG 4  // pdf weights in registers (config 5, same box: 8 / 4 / 0 -> 274 / 276 / 271 Msamples/s)
 #endif
 #ifndef RT_GEN_XREG
-#define RT_GEN_XREG 2  // explicit albedos in registers
+#define RT_GEN_XREG 1  // explicit albedos in registers
 #endif
 constexpr int kWReg = RT_GEN_WREG, kXReg = RT_GEN_XREG;
 template <int kN>
