@@ -132,6 +132,7 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
+  int32_t tail_left;         // chain launches: raised priority in the tail for whole pixels with this many samples left (0: off)
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
@@ -1020,7 +1021,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     const uint64_t wait = __ballot(mode == kWait);
     if ((trav | wait) == 0) break;
     if (kMode == 2) {  // a wave holding a critical chain (kItemCrit) issues ahead of the others on its SIMD
-      const bool c = __ballot(crit && mode != kExit) != 0ull;
+      // (and, once the launch's items ran out for this wave -- a lane has left -- one holding a whole pixel
+      // with at least tail_left samples to go: longest remaining work first)
+      const bool tail = V.tail_left > 0 && __ballot(mode == kExit) != 0ull;
+      const bool c = __ballot(mode != kExit && (crit || (tail && (seg & kItemUnsplit) && spp - s >= V.tail_left))) != 0ull;
       if (c != wave_crit) {
         wave_crit = c;
         if (c) __builtin_amdgcn_s_setprio(1);

@@ -586,6 +586,7 @@ struct Config {
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
   bool order_draws = false;  // chain items start in order of pre-pass draws, not cost (chain_plan_kernel)
   float crit = 0.0f;         // chain lane items of >= crit x c* per segment: raised wave priority (0: off)
+  float tail_left = 0.0f;    // ... and in a wave's tail, whole pixels with >= this share of spp left (0: off)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -615,6 +616,7 @@ struct Config {
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
     c.order_draws = env_flag("RT_ORDER_DRAWS", c.order_draws);
     c.crit = env_float("RT_CRIT", c.crit);
+    c.tail_left = env_float("RT_TAIL_LEFT", c.tail_left);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -1364,6 +1366,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
+  V.tail_left = cfg.tail_left > 0.0f ? (int32_t)ceilf(cfg.tail_left * (float)V.S.cam.spp) : 0;
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
