@@ -984,6 +984,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   int mode = kWait;
 #ifdef RT_LOOP_STATS
   uint64_t st_cyc[2] = {0, 0}, st_last = 0, st_it[2] = {0, 0}, st_lanes[2] = {0, 0}, st_live = 0;
+  uint64_t st_step[4] = {0, 0, 0, 0};  // wave-steps, their stepping lanes, wave-steps running the sphere block, leaf lanes
   int st_kind = 0;
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
@@ -1057,11 +1058,23 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       for (;;) {
         if (mode == kTrav) {
 #pragma unroll
-          for (int u = 0; u < kSteps; u++)
+          for (int u = 0; u < kSteps; u++) {
+#ifdef RT_LOOP_STATS
+            {  // per wave-step: stepping lanes, and whether (and for how many lanes) the sphere block runs
+              bool at_leaf = false;
+              if (mode == kTrav) at_leaf = (__float_as_uint(it_q1(items9, V.n_items9_alloc, L.cur >> 4).w) & kLeaf9) != 0u;
+              const uint64_t stepping = __ballot(mode == kTrav), lm = __ballot(at_leaf);
+              if (stepping) {
+                st_step[0]++, st_step[1] += (uint32_t)__popcll(stepping);
+                if (lm) st_step[2]++, st_step[3] += (uint32_t)__popcll(lm);
+              }
+            }
+#endif
             if (mode == kTrav) {
               if (kMode == 1) px_steps++;  // work-item cost (the LPT pre-pass)
               if (trav_step_v9(items9, na, n9, L, tmin)) mode = kWait;
             }
+          }
         }
         const uint64_t t2 = __ballot(mode == kTrav), w2 = __ballot(mode == kWait);
         const int batch2 = min(V.shade_batch, (3 * (int)__popcll(t2 | w2) + 3) / 4);
@@ -1260,6 +1273,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     atomicAdd(o + 4, (unsigned long long)st_lanes[1]);
     atomicAdd(o + 5, (unsigned long long)st_cyc[1]);
     atomicAdd(o + 6, (unsigned long long)st_live);
+    if (kMode == 2)
+      for (int q = 0; q < 4; q++) atomicAdd(V.loop_stats + 24 + q, (unsigned long long)st_step[q]);
   }
 #endif
   if (kMode == kMigMode && V.mig_live > 0) {

@@ -1430,6 +1430,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
               "lanes/pass %.1f cycles %.1f%% | live lanes/iter %.1f\n", r[0], r[0] ? (double)r[1] / r[0] : 0.0,
               100.0 * r[2] / cyc, r[3], r[3] ? (double)r[4] / r[3] : 0.0, 100.0 * r[5] / cyc,
               (r[0] + r[3]) ? (double)r[6] / (r[0] + r[3]) : 0.0);
+      const unsigned long long *w = q + 24;
+      fprintf(stderr, "[rtc] loop stats (cumulative): wave-steps %llu, stepping lanes/step %.1f; steps running the sphere "
+              "block %.1f%%, leaf lanes in those %.2f\n", w[0], w[0] ? (double)w[1] / w[0] : 0.0,
+              w[0] ? 100.0 * w[2] / w[0] : 0.0, w[2] ? (double)w[3] / w[2] : 0.0);
     }
 #endif
 

@@ -3,7 +3,7 @@
 #   TAG=r03a CFG="--scene 1 --width 1200 --spp 1000" bash scripts/gpu_profile.sh
 # 1. [SKIP_BENCH=1 skips] the bench line of the configuration (N=1, CPU baseline);
 # 2. rocprofv3 --kernel-trace --stats over bench.py (--steps 2 --warmup 1: 3 frames);
-# 3. four rocprofv3 --pmc passes (counters in separate runs, kernel-trace only), 1 frame each;
+# 3. five rocprofv3 --pmc passes (counters in separate runs, kernel-trace only), 1 frame each;
 # 4. scripts/pmc_summary.py -> gpurun_out/${TAG}_pmc_<config key>.json, per frame, stamped with the
 #    library's rt_build_id (copy it to profiles/<round>/ for bench.py to attach).
 # Every GPU step has its own time limit; a failing step ends the script.
@@ -30,7 +30,8 @@ s = rtc.Scene.preset(a.scene, a.width, 1, 1, substitute_earth=True)
 print(f"s{a.scene}_{s.width}x{s.height}_{a.spp}spp_d{a.depth}_n1", s.width * s.height * a.spp, rtc.build_id())
 PY
 )
-echo "config $KEY samples/frame $SAMPLES build $BID"
+BOX=$(python3 -c "import sys, json; sys.path.insert(0, 'ray-tracing-c_amd'); import rtc; print(json.dumps(rtc.box_identity()))")
+echo "config $KEY samples/frame $SAMPLES build $BID box $BOX"
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 900 python3 bench.py $CFG
 step stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o run -- \
     python3 bench.py $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-parity
@@ -41,7 +42,10 @@ step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_AC
     --output-format csv -d gpurun_out/${TAG}_pmc_sq2 -o run -- python3 bench.py $A
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- python3 bench.py $A
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write -o run -- python3 bench.py $A
-python3 scripts/pmc_summary.py gpurun_out/${TAG}_pmc_${KEY}.json --build-id "$BID" --config "$KEY" --samples-per-frame "$SAMPLES" \
+# the L2's atomics and its memory-side requests (the chain protocol's cross-XCD words; box-to-box comparison)
+step pmc_atom 600 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum \
+    --output-format csv -d gpurun_out/${TAG}_pmc_atom -o run -- python3 bench.py $A
+python3 scripts/pmc_summary.py gpurun_out/${TAG}_pmc_${KEY}.json --build-id "$BID" --config "$KEY" --samples-per-frame "$SAMPLES" --box "$BOX" \
     --stats gpurun_out/${TAG}_stats --stats-frames 3 --pmc-frames 1 \
-    gpurun_out/${TAG}_pmc_sq1 gpurun_out/${TAG}_pmc_sq2 gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write
+    gpurun_out/${TAG}_pmc_sq1 gpurun_out/${TAG}_pmc_sq2 gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write gpurun_out/${TAG}_pmc_atom
 find gpurun_out/${TAG}_stats -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats_${KEY}.csv \;

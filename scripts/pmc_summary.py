@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--stats-frames", type=int, default=1)
     ap.add_argument("--pmc-frames", type=int, default=1)
+    ap.add_argument("--box", default="{}", help="JSON: the box the passes ran on (rtc.box_identity)")
     ap.add_argument("pmc", nargs="*")
     a = ap.parse_intermixed_args()
     res = collections.defaultdict(dict)
@@ -82,7 +83,7 @@ def main():
             e["write_bytes"] = c["WRITE_SIZE"] * 1024 / F
         if "fetch_bytes" in e and "write_bytes" in e:
             e["traffic_bytes_per_sample"] = (e["fetch_bytes"] + e["write_bytes"]) / S
-    out = {"build_id": a.build_id, "config": a.config, "samples_per_frame": S, "stats_dir": a.stats,
+    out = {"build_id": a.build_id, "config": a.config, "box": json.loads(a.box), "samples_per_frame": S, "stats_dir": a.stats,
            "stats_frames": a.stats_frames, "pmc_passes": a.pmc, "pmc_frames": F,
            "note": "per-frame figures: totals / frames; bytes per frame", "kernels": res}
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
