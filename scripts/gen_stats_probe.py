@@ -1,4 +1,5 @@
-"""Counters of the general kernel's batched loop (build with -DRT_GEN_STATS, RT_DEBUG=1), summarised.
+"""Counters of the general kernel's batched loop (build with -DRT_DIAG -DRT_GEN_STATS, RT_DEBUG=1), summarised.
+    scripts/ab_variant.sh gstats "-DRT_DIAG -DRT_GEN_STATS"
     RTC_LIB=ab/gstats.so RT_DEBUG=1 python scripts/gen_stats_probe.py [SCENE] [WIDTH] [SPP]
 Prints the library's "[rtc] gen stats:" line (stderr) and the derived shares: cycles by loop phase,
 lanes per trace / shade iteration, entry kinds per traversal step, materials and textures shaded."""

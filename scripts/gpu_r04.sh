@@ -43,6 +43,11 @@ ab() {  # ab "<entries>" "<bench args>"
 [ -n "${AB:-}" ] && ab "$AB" "${BENCH_ARGS:-}"
 # AB7: the same for config 5 (scene 7, 1000x1000x1000 spp, one frame)
 [ -n "${AB7:-}" ] && ab "$AB7" "--scene 7 --width 1000 --steps 1 --warmup 1"
+if [ "${LOOPSTATS:-0}" = 1 ]; then  # the loop-stats build (ab/loopstats.so, -DRT_DIAG -DRT_LOOP_STATS): phase split
+  RTC_LIB=$GRAFT_REPO_ROOT/ab/loopstats.so RT_DEBUG=1 timeout -k 10 300 python bench.py --steps 1 --warmup 0 \
+      --no-cpu-baseline --no-parity > gpurun_out/${TAG}_loopstats.log 2>&1
+  echo "== loopstats rc=$?"; grep "\[rtc\] \(loop\|chain launch ms\)" gpurun_out/${TAG}_loopstats.log
+fi
 [ "${S7:-0}" = 1 ] && step s7_bench 300 python bench.py --no-cpu-baseline --scene 7 --width 1000 --steps 1 --warmup 1
 [ "${SHARD:-0}" = 1 ] && step shard 400 python -u scripts/shard_probe.py ${WORLDS:-2,4,8} all 1000
 # SHARD_ENVS="RT_CHAIN_PAD=1.2;...": the shard probe on the diagnostic build under each setting

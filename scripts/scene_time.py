@@ -3,7 +3,8 @@ RTC_LIB picks the build), with the image checked identical across settings.
     python scripts/scene_time.py SCENE WIDTH SPP "ENV;ENV;..." [REPS]
 ENV is comma-separated K=V pairs ("" = defaults), e.g.  7 1000 256 ";RT_GEN_RARE=1;RT_GEN_RARE=16"
 The library reads its RT_* configuration when a scene is uploaded, so each setting gets a fresh
-upload of the same scene."""
+upload of the same scene.  The A/B switches are read by the diagnostic build only (librtc_amd_diag.so,
+used here unless RTC_LIB names another build)."""
 import hashlib
 import os
 import sys
@@ -16,7 +17,9 @@ import rtc  # noqa: E402
 scene, width, spp = (int(x) for x in sys.argv[1:4])
 settings = sys.argv[4].split(";") if len(sys.argv) > 4 else [""]
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 2
-sc = rtc.Scene.preset(scene, width, spp, 50, substitute_earth=True)
+diag = rtc.use_diag(not os.environ.get("RTC_LIB"))
+with diag:
+    sc = rtc.Scene.preset(scene, width, spp, 50, substitute_earth=True)
 st = torch.cuda.current_stream()
 buf = torch.empty((sc.height, sc.width, 3), dtype=torch.uint8, device="cuda")
 base = {k: os.environ.get(k) for s in settings for k in (kv.split("=")[0] for kv in s.split(",") if kv)}
@@ -30,7 +33,8 @@ for s in settings:
     for kv in (x for x in s.split(",") if x):
         k, v = kv.split("=", 1)
         os.environ[k] = v
-    ds = rtc.DeviceScene(sc, 0)
+    with diag:
+        ds = rtc.DeviceScene(sc, 0)
     ds.render_rows_async(0, 1, sc.height, buf.data_ptr(), st.cuda_stream)  # warm-up
     torch.cuda.synchronize()
     best, kbest = 1e30, 1e30
