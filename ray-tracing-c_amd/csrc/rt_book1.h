@@ -107,7 +107,7 @@ constexpr uint32_t kItemUnsplit = 0x80000000u;  // ch_items[].y: K == 1, the who
 constexpr uint32_t kItemCrit = 0x40000000u;     //   ... a critical lane item: its wave runs at raised priority
 constexpr uint64_t kEndEnded = 1ull << 63;      // end word: the segment's chain has ended
 constexpr uint64_t kEndNoLink = 1ull << 62;     //   ... without coupling (pixel complete / list full)
-constexpr uint32_t kRecFill = 0xffffffffu;      // ch_end before the record's sample starts
+constexpr uint32_t kRecFill = 0xffffffffu;      // ch_end before the record is written
 constexpr uint32_t kNoTarget = 0xff000000u;     // coupling cursor (t << 24 | c): none
 constexpr int kMaxSeg = 255;                    // t fits 8 bits (host: chain planner caps K lower)
 RT_D uint32_t end_n(uint64_t w) { return (uint32_t)(w >> 32) & 0x3fffffffu; }
@@ -123,9 +123,6 @@ RT_D uint64_t ld_rel64(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC
 RT_D void st_rel(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D void st_rel64(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D uint32_t ld_acq(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
-RT_D uint64_t ld_acq64(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
-// a segment's end word: release, so that a reader that sees it sees the segment's flip word as final
-RT_D void st_end64(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT); }
 
 struct Book1View {
   DScene S;                  // full scene (global memory): sphere aux data, camera
@@ -152,8 +149,7 @@ struct Book1View {
   const uint32_t *ch_n_items;
   uint64_t *ch_seg;          // segment end words (0: running)
   float4 *ch_col;            // records: colour, end offset (bits)
-  uint32_t *ch_end;          // records: start offset, published as the sample starts (kRecFill until then)
-  uint64_t *ch_flip;         // per segment slot: parity flips asked of / made by the segment (chain_flip_word)
+  uint32_t *ch_end;          // records: end offset (kRecFill until written)
   float4 *ch_acc0;           // per pixel: segment 0's colour sum when it coupled
   uint32_t *seg_time;        // diagnostic (RT_PX_TIME=1): per segment {start, end, migrated} at end0 + k
   const ChainCont *ch_cont;  // continuation launch: items from here (else null)
@@ -561,77 +557,30 @@ RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, f
 }
 
 // ---------------------------------------------------------------- chain protocol (kMode 2)
-// ---------------------------------------------------------------- parity flips
-// Most samples draw an even number of pcg32 values (2 for the pixel jitter, 2 per Lambertian bounce);
-// metal (3 per rejection try) and glass (1) make odd counts.  Segments start at even offsets, so once
-// the true chain has taken an odd number of odd-count samples it runs on odd offsets, and two chains
-// of different parity meet only after one of them takes another odd-count sample -- with odd counts
-// rare, a "parity trap": the chain carrying the true stream passes its successor's start and runs on
-// alone, possibly to the pixel's end.  The fix: a chain past its successor's start by
-// kTrapSamples samples' worth of draws, whose successor's next record starts on the other parity, asks
-// the successor to skip one draw (req += 1); the successor does so at its next sample boundary (done +=
-// 1, off = its offset after the skip).  Its later records then run on the asking chain's parity, and
-// the two couple as usual once the asking chain passes the skip (the scan steps over the records before
-// it: every record carries its own start).  Exact: a segment that skips a draw is just a chain started
-// at another offset -- with one caveat the walk and the fold handle: if the true chain nevertheless
-// enters the segment at a record before the skip (the asking chain's own parity flipped back by an
-// odd-count sample), the records from the skip on are not its continuation, so the true chain breaks
-// there (the pixel finishes through a continuation item).  One flip per segment.
-// Flip word (per segment slot): bits 0-31 the offset after the skip, 32-39 asked, 40-47 made, 48-63 the
-// first record after the skip.
-constexpr uint32_t kTrapSamples = 24;
-RT_D uint32_t flip_off(uint64_t f) { return (uint32_t)f; }
-RT_D uint32_t flip_req(uint64_t f) { return (uint32_t)(f >> 32) & 0xffu; }
-RT_D uint32_t flip_done(uint64_t f) { return (uint32_t)(f >> 40) & 0xffu; }
-RT_D uint32_t flip_rec(uint64_t f) { return (uint32_t)(f >> 48); }
-// Records of segment t usable by a true chain entering it at record c: up to n, or -- the segment
-// flipped after record c -- up to the flip (broken: the true chain does not go on in this segment).
-RT_D uint32_t flip_limit(const Book1View &V, const ChainPx &P, uint32_t t, uint32_t c, uint32_t n, bool &broken) {
-  broken = false;
-  if (!V.ch_flip || t == 0u) return n;
-  const uint64_t f = ld_rel64(&V.ch_flip[P.end0 + t]);
-  if (flip_done(f) == 0u || c >= flip_rec(f)) return n;
-  broken = true;
-  return flip_rec(f) < n ? flip_rec(f) : n;
-}
-RT_D uint32_t trap_draws(const ChainPx &P, uint32_t spp) {  // kTrapSamples samples in draws (>= 64)
-  const uint64_t d = (uint64_t)kTrapSamples * P.seg_len * P.K / spp;
-  return d < 64u ? 64u : (uint32_t)d;
-}
-RT_D uint32_t uni32(uint32_t v) {  // wave-uniform (lane 0's value) on the device
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-#else
-  return v;
-#endif
-}
-
 // Coupling cursor: successor segment t << 24 | record c.
 constexpr uint32_t kCurRec = 0xffffffu;
 
 // Coupling scan of chain k at its sample boundary x: does a successor record start at x?  tc = the
-// cursor (record c of segment t), st = the start offset of record c (ch_end: records publish their
-// start as their sample begins, so a successor that skipped a draw -- chain_flip -- leaves no gap the
-// scan could mistake for a sample start).  Returns true when coupled (tc then names the record that
-// starts at x).  Bounded work per call; a record not started yet, or a successor still running past its
-// last record, is looked at again next time.
+// cursor, st = the start offset of its record.  Returns true when coupled (tc then names the record
+// that starts at x).  Bounded work per call; a record not yet written, or a successor still running
+// past its last record, is looked at again next time.
 RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t x, uint32_t &tc, uint32_t &st) {
   for (int it = 0; it < 24; it++) {
     const uint32_t t = tc >> 24, c = tc & kCurRec;
     if (t >= P.K) return false;  // no successor (kNoTarget)
     if (st > x) return false;  // the successor's next sample starts beyond x
     if (st == x) return true;
-    if (c + 1u < seg_cap(P, t)) {  // st < x: step to record c + 1
-      const uint32_t e = ld_rel(&V.ch_end[rec_index(P, t, c + 1u)]);
+    if (c < seg_cap(P, t)) {  // st < x: step over record c
+      const uint32_t e = ld_rel(&V.ch_end[rec_index(P, t, c)]);
       if (e != kRecFill) {
         st = e;
         tc = (tc & ~kCurRec) | (c + 1u);
         continue;
       }
     }
-    // record c + 1 has not started: follow the successor's link if it has ended after record c
+    // record c is not there (yet): follow the successor's link if it has ended past its last record
     const uint64_t w = ld_rel64(&V.ch_seg[P.end0 + t]);
-    if (!(w & kEndEnded) || c + 1u < end_n(w)) return false;  // running, or its record c + 1 in flight
+    if (!(w & kEndEnded) || c < end_n(w)) return false;  // running, or its record c still in flight
     if (w & kEndNoLink) {
       tc = kNoTarget;  // it ended without a link: nothing to couple with beyond it
       return false;
@@ -643,7 +592,7 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_
     }
     uint32_t s2 = seg_start(P, t2);
     if (c2 > 0) {
-      s2 = ld_rel(&V.ch_end[rec_index(P, t2, c2)]);
+      s2 = ld_rel(&V.ch_end[rec_index(P, t2, c2 - 1u)]);
       if (s2 == kRecFill) return false;
     }
     tc = (t2 << 24) | c2;
@@ -661,60 +610,16 @@ RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint
   if (w & kEndNoLink) return true;  // segment 0 completed the pixel
   uint32_t total = end_n(w), t = end_t(w), c = end_c(w);
   for (uint32_t it = 0; it < P.K; it++) {
-    bool broken;
-    if (t == k) {
-      (void)flip_limit(V, P, k, c, n, broken);
-      return broken || total + (n - c) >= spp;  // (entered before its own flip: its later records are no use)
-    }
+    if (t == k) return total + (n - c) >= spp;
     if (t > k) return true;  // the true chain skips this chain
-    w = ld_acq64(&V.ch_seg[P.end0 + t]);  // (acquire: the segment's flip word is final once it has ended)
+    w = ld_rel64(&V.ch_seg[P.end0 + t]);
     if (!(w & kEndEnded)) return false;
-    const uint32_t lim = flip_limit(V, P, t, c, end_n(w), broken);
-    if (broken || (w & kEndNoLink)) return true;  // the true chain ends (or breaks) before this chain
-    total += lim - c;
+    if (w & kEndNoLink) return true;  // the true chain ends (or breaks) before this chain
+    total += end_n(w) - c;
     if (total >= spp) return true;
     t = end_t(w), c = end_c(w);
   }
   return false;
-}
-
-// Chain k at its boundary x, not coupled: ask the successor for a flip when trapped (one writer).
-RT_D void chain_flip_ask(const Book1View &V, const ChainPx &P, uint32_t k, uint32_t x, uint32_t tc, uint32_t st,
-                         uint32_t spp) {
-  if ((tc >> 24) != k + 1u || k + 1u >= P.K || st <= x || !((x ^ st) & 1u)) return;
-  const uint32_t d = trap_draws(P, spp);
-  if (x < seg_start(P, k + 1u) + d) return;
-  uint64_t *fw = &V.ch_flip[P.end0 + k + 1u];
-  const uint64_t f = ld_rel64(fw);
-  const uint32_t req = flip_req(f), done = flip_done(f);
-  if (req != 0u || done != 0u) return;  // (one flip per segment)
-  __hip_atomic_fetch_add(fw, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Before sample s of segment k >= 1 (after its boundary found more work): make a flip its predecessor
-// asked for, then publish the sample's start offset (record s).  Wave-uniform callers: every lane calls
-// it (the stream state stays uniform), writer only in lane 0.
-RT_D void chain_sample_begin(const Book1View &V, int64_t pix, uint32_t seg, uint32_t s, Pcg32 &g, bool writer) {
-  if ((seg & kItemUnsplit) || seg == 0u) return;
-  const ChainPx &P = V.ch_px[pix];
-  const uint32_t spp = (uint32_t)V.S.cam.spp;
-  if (V.ch_flip && (s & 3u) == 0u && 2u * s * P.K >= spp) {  // (asks come after the predecessor reached this segment)
-    uint64_t *fw = &V.ch_flip[P.end0 + seg];
-    const uint64_t f = ld_rel64(fw);
-    if (uni32(flip_req(f)) > uni32(flip_done(f))) {
-      (void)g.next();  // skip one draw: this segment's later samples run on the other parity
-      if (writer) {
-        uint64_t old = f;
-        for (;;) {
-          const uint64_t nw = (old & (0xffull << 32)) | ((uint64_t)(flip_done(old) + 1u) << 40) | ((uint64_t)s << 48) | g.n;
-          if (__hip_atomic_compare_exchange_strong(fw, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT))
-            break;
-        }
-      }
-    }
-  }
-  if (writer) st_rel(&V.ch_end[rec_index(P, seg, s)], g.n);
 }
 
 // A chain's sample boundary (kMode 2): before each sample.  seg = the item's segment word; s = the
@@ -750,34 +655,34 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
   if (k == 0 && s >= spp) {  // the head reached the end before coupling
     if (writer) {
       write_pixel(out + pix * 3, acc, (int)spp);
-      st_end64(&V.ch_seg[P.end0], end_word(s, false, 0u));
+      st_rel64(&V.ch_seg[P.end0], end_word(s, false, 0u));
     }
     return true;
   }
   if (k > 0 && s >= seg_cap(P, k)) {  // the list is full
-    if (writer) st_end64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
+    if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
   if (chain_couple(V, P, k, x, tc, st)) {
     if (writer) {
       if (k == 0) V.ch_acc0[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-      st_end64(&V.ch_seg[P.end0 + k], end_word(s, true, tc));
+      st_rel64(&V.ch_seg[P.end0 + k], end_word(s, true, tc));
     }
     return true;
   }
   if (k > 0 && s >= P.check && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
-    if (writer) st_end64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
+    if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
-  if (writer && V.ch_flip) chain_flip_ask(V, P, k, x, tc, st, spp);
   return false;
 }
 
-// Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it); its start offset
-// was published as the sample began (chain_sample_begin).
+// Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it).
 RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, f3 col, uint32_t x_end) {
   const ChainPx &P = V.ch_px[pix];
-  V.ch_col[rec_index(P, k, c)] = make_float4(col.x, col.y, col.z, u2f(x_end));
+  const uint32_t at = rec_index(P, k, c);
+  V.ch_col[at] = make_float4(col.x, col.y, col.z, u2f(x_end));
+  st_rel(&V.ch_end[at], x_end);
 }
 
 // A chain's start: stream position, and its coupling cursor on its successor.
@@ -826,7 +731,6 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       tc = (uint32_t)__builtin_amdgcn_readfirstlane((int)tc);
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
       if (__builtin_amdgcn_readfirstlane((int)done)) break;
-      chain_sample_begin(V, pix, seg, s, g, lane0);
     } else if (s == (uint32_t)cam.spp) {
       break;
     }
@@ -1313,7 +1217,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         need_sample = false;
         break;
       }
-      if (kMode == 2) chain_sample_begin(V, pix, seg, (uint32_t)s, g, true);
       // camera ray (src/raytracing.c:96-122)
       const int jj = pix / W, i = pix - jj * W, j = V.row0 + jj * V.row_stride;
       const f3 pixel_pos = add(add(ld3(cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
@@ -1405,13 +1308,12 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     acc = mk(a0.x, a0.y, a0.z);
     total = end_n(w);
     t = end_t(w), c = end_c(w);
-    o = c == 0 ? seg_start(P, t) : V.ch_end[rec_index(P, t, c)];  // (the start of record c)
+    o = c == 0 ? seg_start(P, t) : V.ch_end[rec_index(P, t, c - 1u)];
   }
   while (linked && total < spp) {
     if (t == 0 || t >= P.K) break;  // (never: links point forward)
     w = V.ch_seg[P.end0 + t];
-    bool broken;
-    const uint32_t n = flip_limit(V, P, t, c, end_n(w), broken);  // (entered before a flip: up to it)
+    const uint32_t n = end_n(w);
     const uint32_t m = n > c ? min(n - c, spp - total) : 0u;
     for (uint32_t b = 0; b < m; b += 64) {
       float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1423,7 +1325,7 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     }
     total += m;
     if (total >= spp) break;
-    if (broken || !(w & kEndEnded) || (w & kEndNoLink)) {
+    if (!(w & kEndEnded) || (w & kEndNoLink)) {
       linked = false;
       break;
     }

@@ -351,7 +351,7 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
                                                          uint32_t *cnt, ChainModel m, b1::ChainPx *px,
-                                                         uint64_t *seg, uint64_t *flip, uint32_t *kk, uint32_t *split) {
+                                                         uint64_t *seg, uint32_t *kk, uint32_t *split) {
   __shared__ uint32_t h[256];
   __shared__ unsigned long long wwork;
   for (int k = threadIdx.x; k < 256; k += blockDim.x) h[k] = 0;
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
         P.cap_last = cap_last;
         P.pad = 0u;
         px[p] = P;
-        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull, flip[e0 + k] = 0ull;
+        for (uint32_t k = 0; k < n_end; k++) seg[e0 + k] = 0ull;
         split[atomicAdd(&cnt[kCnSplit], 1u)] = (uint32_t)p;
       }
     }
@@ -510,8 +510,7 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
   for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = make_uint2((uint32_t)(val[i] >> 32), (uint32_t)val[i]);
 }
 
-// ch_end (the records' start offsets) = kRecFill for the planned records; cnt[kCnFilled] = the end of
-// the filled range.
+// ch_end = kRecFill for the planned records; cnt[kCnFilled] = the end of the filled range.
 __global__ void chain_fill_kernel(uint32_t *cnt, uint32_t *ch_end, uint32_t cap) {
   const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
@@ -588,7 +587,6 @@ struct Config {
   bool order_draws = false;  // chain items start in order of pre-pass draws, not cost (chain_plan_kernel)
   float crit = 0.0f;         // chain lane items of >= crit x c* per segment: raised wave priority (0: off)
   float tail_left = 0.0f;    // ... and in a wave's tail, whole pixels with >= this share of spp left (0: off)
-  bool chain_flip = false;   // parity flips of trapped successors (rt_book1.h: chain_flip_ask; A/B)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -619,7 +617,6 @@ struct Config {
     c.order_draws = env_flag("RT_ORDER_DRAWS", c.order_draws);
     c.crit = env_float("RT_CRIT", c.crit);
     c.tail_left = env_float("RT_TAIL_LEFT", c.tail_left);
-    c.chain_flip = env_flag("RT_CHAIN_FLIP", c.chain_flip);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -704,7 +701,7 @@ struct rt_device_scene {
   uint32_t *ch_cnt = nullptr, *ch_k = nullptr, *ch_split = nullptr;
   b1::ChainPx *ch_px = nullptr;
   uint2 *ch_items = nullptr;
-  uint64_t *ch_seg = nullptr, *ch_wave_key = nullptr, *ch_flip = nullptr;
+  uint64_t *ch_seg = nullptr, *ch_wave_key = nullptr;
   float4 *ch_acc0 = nullptr;
   b1::ChainCont *ch_cont = nullptr;
   uint32_t ch_seg_cap = 0;
@@ -1017,12 +1014,11 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     const int kmax = cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave;
     const size_t nitem = npix * (size_t)kmax, nseg = npix * (size_t)kmax;
     d->ch_seg_cap = nseg < 0xffffffffu ? (uint32_t)nseg : 0xffffffffu;
-    const size_t cs[10] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
-                           npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
-                           nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont),
-                           nseg * sizeof(uint64_t)};
-    size_t co[10], ct = 0;
-    for (int k = 0; k < 10; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
+    const size_t cs[9] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
+                          npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
+                          nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont)};
+    size_t co[9], ct = 0;
+    for (int k = 0; k < 9; k++) co[k] = ct, ct = align_up(ct + cs[k], 256);
     HIP_OK(hipMalloc(&d->ch_arena, ct));
     char *c = (char *)d->ch_arena;
     d->ch_cnt = (uint32_t *)(c + co[0]);
@@ -1034,7 +1030,6 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_wave_key = (uint64_t *)(c + co[6]);
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
-    d->ch_flip = (uint64_t *)(c + co[9]);
     if (cfg.px_time) {
       HIP_OK(hipMalloc(&d->seg_time, nseg * 3 * sizeof(uint32_t)));
       V.seg_time = d->seg_time;
@@ -1338,7 +1333,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   uint32_t *end = (uint32_t *)(col + d->ch_rec_cap);
   hipLaunchKernelGGL(chain_params_kernel, dim3(1), dim3(64), 0, st, sums, d->ch_cnt, m);
   hipLaunchKernelGGL(chain_plan_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, d->draw_out, n, d->ch_cnt, m, d->ch_px,
-                     d->ch_seg, d->ch_flip, d->ch_k, d->ch_split);
+                     d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, cfg.order_draws ? d->draw_out : d->lpt_cost, n,
                      d->ch_cnt, d->ch_k, d->ch_items, d->ch_wave_key);
@@ -1359,7 +1354,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.ch_seg = d->ch_seg;
   V.ch_col = col;
   V.ch_end = end;
-  V.ch_flip = cfg.chain_flip ? d->ch_flip : nullptr;
   V.ch_acc0 = d->ch_acc0;
   V.ch_cont = nullptr;
   V.ch_n_cont = nullptr;

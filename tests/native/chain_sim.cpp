@@ -133,7 +133,6 @@ int main(int argc, char **argv) {
   }
   col.assign(rec, make_float4(0, 0, 0, 0));
   endw.assign(rec, b1::kRecFill);
-  std::vector<uint64_t> flip(seg.size(), 0ull);
   std::vector<uint32_t> mig(b1::kMigWords, 0u);
   b1::Book1View V;
   memset(&V, 0, sizeof V);
@@ -142,7 +141,6 @@ int main(int argc, char **argv) {
   V.ch_seg = seg.data();
   V.ch_col = col.data();
   V.ch_end = endw.data();
-  V.ch_flip = flip.data();
   V.ch_acc0 = acc0.data();
   V.mig = mig.data();
   V.mig_epoch = 1u;
@@ -164,7 +162,6 @@ int main(int argc, char **argv) {
       live.pop_back();
       continue;
     }
-    b1::chain_sample_begin(V, c.pix, c.seg, c.s, c.g, true);
     const f3 color = sample(view, c.pix, c.g);
     samples++;
     if (!(c.seg & b1::kItemUnsplit) && c.seg > 0)
@@ -185,7 +182,7 @@ int main(int argc, char **argv) {
     }
     f3 acc = mk(acc0[p].x, acc0[p].y, acc0[p].z);
     uint32_t total = b1::end_n(w), t = b1::end_t(w), c = b1::end_c(w);
-    uint32_t o = c == 0 ? b1::seg_start(P, t) : endw[b1::rec_index(P, t, c)];
+    uint32_t o = c == 0 ? b1::seg_start(P, t) : endw[b1::rec_index(P, t, c - 1)];
     for (;;) {
       if (t == 0 || t >= P.K) {
         fprintf(stderr, "pixel %u: bad link %u\n", p, t);
@@ -196,15 +193,14 @@ int main(int argc, char **argv) {
         fprintf(stderr, "pixel %u: segment %u never ended\n", p, t);
         return 3;
       }
-      bool broken;
-      const uint32_t n = b1::flip_limit(V, P, t, c, b1::end_n(w), broken);
+      const uint32_t n = b1::end_n(w);
       for (uint32_t q = c; q < n && total < (uint32_t)spp; q++) {
         const float4 r = col[b1::rec_index(P, t, q)];
         acc = add(acc, mk(r.x, r.y, r.z));
         o = b1::f2u(r.w);
         total++;
       }
-      if (total >= (uint32_t)spp || broken || (w & b1::kEndNoLink)) break;
+      if (total >= (uint32_t)spp || (w & b1::kEndNoLink)) break;
       t = b1::end_t(w), c = b1::end_c(w);
     }
     if (total < (uint32_t)spp) {  // continuation: the true chain from (o, total, acc)
@@ -219,10 +215,8 @@ int main(int argc, char **argv) {
   FILE *f = fopen(argv[5], "wb");
   fwrite(img.data(), 1, img.size(), f);
   fclose(f);
-  long flips = 0;
-  for (uint64_t f : flip) flips += (long)b1::flip_done(f);
-  printf("%d %d split=%zu chains=%zu samples=%ld (x%.3f) continuations=%d flips=%ld\n", W, H, split.size(),
-         chains.size(), samples, (double)samples / ((double)npix * spp), n_cont, flips);
+  printf("%d %d split=%zu chains=%zu samples=%ld (x%.3f) continuations=%d\n", W, H, split.size(),
+         chains.size(), samples, (double)samples / ((double)npix * spp), n_cont);
   rt_flat_free(s);
   return 0;
 }
