@@ -104,7 +104,6 @@ struct MigRec {       // 64 B
   uint32_t pad[2];
 };
 constexpr uint32_t kItemUnsplit = 0x80000000u;  // ch_items[].y: K == 1, the whole pixel
-constexpr uint32_t kItemCrit = 0x40000000u;     //   ... a critical lane item: its wave runs at raised priority
 constexpr uint64_t kEndEnded = 1ull << 63;      // end word: the segment's chain has ended
 constexpr uint64_t kEndNoLink = 1ull << 62;     //   ... without coupling (pixel complete / list full)
 constexpr uint32_t kRecFill = 0xffffffffu;      // ch_end before the record is written
@@ -132,7 +131,6 @@ struct Book1View {
   int32_t row0, row_stride, n_rows;
   int32_t *work_counter;     // zeroed before each launch
   int32_t shade_batch;       // shade once this many lanes of a wave are waiting
-  int32_t tail_left;         // chain launches: raised priority in the tail for whole pixels with this many samples left (0: off)
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
@@ -998,7 +996,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   g.inc = 0;
   g.n = 0;
   uint32_t seg = kItemUnsplit, tc = kNoTarget, st = 0;  // chain render: segment, coupling cursor
-  bool crit = false, wave_crit = false;  // chain render: this lane's item is critical; the wave's priority is raised
   f3 acc = mk(0, 0, 0);
   Record R;
   R.r0 = R.r1 = 0;
@@ -1021,17 +1018,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     const uint64_t trav = __ballot(mode == kTrav);
     const uint64_t wait = __ballot(mode == kWait);
     if ((trav | wait) == 0) break;
-    if (kMode == 2) {  // a wave holding a critical chain (kItemCrit) issues ahead of the others on its SIMD
-      // (and, once the launch's items ran out for this wave -- a lane has left -- one holding a whole pixel
-      // with at least tail_left samples to go: longest remaining work first)
-      const bool tail = V.tail_left > 0 && __ballot(mode == kExit) != 0ull;
-      const bool c = __ballot(mode != kExit && (crit || (tail && (seg & kItemUnsplit) && spp - s >= V.tail_left))) != 0ull;
-      if (c != wave_crit) {
-        wave_crit = c;
-        if (c) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-    }
     // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
@@ -1177,7 +1163,6 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         acc = mk(0.0f, 0.0f, 0.0f);
         s = 0;
         seg = kItemUnsplit;
-        crit = false;
         tc = kNoTarget;
         if (kMode == 2 && cont) {  // the true chain on from an exact position (chain_fold_kernel)
           const ChainCont c = V.ch_cont[item];
@@ -1188,8 +1173,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         } else if (kMode == 2) {
           const uint2 it = V.ch_items[item + work_offset];
           pix = (int32_t)it.x;
-          seg = it.y & ~kItemCrit;
-          crit = (it.y & kItemCrit) != 0u;
+          seg = it.y;
         } else {
           pix = (int32_t)item;  // (lane launches: low spp / small images, in pixel order)
         }

@@ -332,8 +332,6 @@ struct ChainModel {
   int width, smooth;    // launch row width; draw estimates averaged over +-smooth pixels of the row
   float est_scale;      // stream length estimate x this
   float pad;            // pixels of >= pad_k segments: segments of the planned length over pad x the estimate
-  int order_draws;      // start order by pre-pass draws instead of cost
-  float crit;           // lane items of at least crit x c* per segment run at raised wave priority (0: off)
   int pad_k;
   uint32_t rec_cap;     // records available
   uint32_t seg_cap;     // end words available
@@ -421,12 +419,8 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       }
     }
     if (K == 1) wave = wave && c > 0u;
-    // critical lane items (rt_book1.h: kItemCrit): the longest chains, whose latency sets the tail
-    const bool crit = !wave && m.crit > 0.0f && (float)(c / (uint32_t)K) >= m.crit * __uint_as_float(cnt[kCnCstar]);
-    kk[p] = (uint32_t)K | (wave ? 0x80000000u : 0u) | (crit ? 0x40000000u : 0u);
-    // the start-order key: the item's cost, or (m.order_draws) its pcg32 draws -- a lane chain's
-    // latency follows its bounces (one shading pass each) more than its traversal steps
-    const uint32_t cc = (m.order_draws ? draws[p] : c) / (uint32_t)K;
+    kk[p] = (uint32_t)K | (wave ? 0x80000000u : 0u);
+    const uint32_t cc = c / (uint32_t)K;
     if (wave) {
       atomicAdd(&cnt[kCnWave], (uint32_t)K);
       atomicAdd(&wwork, (unsigned long long)c);
@@ -460,7 +454,6 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
 
 __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk,
                                                             uint2 *items, uint64_t *wave_key) {
-  // (cost: the start-order key chain_plan_kernel bucketed by)
   // two-level: the block's items per bucket are counted in LDS, one global atomic per bucket and
   // block reserves their range (one global atomic per pixel on 256 bucket words serialised: 3 ms
   // for a full frame)
@@ -485,7 +478,7 @@ __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost
     if (p < n) {
       const uint32_t at = base_l[b] + loc;
       for (uint32_t k = 0; k < K; k++) {
-        items[at + k] = make_uint2((uint32_t)p, (K == 1u ? b1::kItemUnsplit : k) | (kk[p] & 0x40000000u ? b1::kItemCrit : 0u));
+        items[at + k] = make_uint2((uint32_t)p, K == 1u ? b1::kItemUnsplit : k);
         if (b == 256u) wave_key[at + k] = ((uint64_t)cc << 32) | (uint32_t)(0xffffffffu - (at + k));
       }
     }
@@ -584,9 +577,6 @@ struct Config {
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
-  bool order_draws = false;  // chain items start in order of pre-pass draws, not cost (chain_plan_kernel)
-  float crit = 0.0f;         // chain lane items of >= crit x c* per segment: raised wave priority (0: off)
-  float tail_left = 0.0f;    // ... and in a wave's tail, whole pixels with >= this share of spp left (0: off)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -614,9 +604,6 @@ struct Config {
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
-    c.order_draws = env_flag("RT_ORDER_DRAWS", c.order_draws);
-    c.crit = env_float("RT_CRIT", c.crit);
-    c.tail_left = env_float("RT_TAIL_LEFT", c.tail_left);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -1314,8 +1301,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.smooth = cfg.chain_smooth;
   m.est_scale = cfg.chain_est;
   m.pad = cfg.chain_pad;
-  m.order_draws = cfg.order_draws ? 1 : 0;
-  m.crit = cfg.crit;
   m.pad_k = cfg.chain_pad_k < 2 ? 2 : cfg.chain_pad_k;
   m.kmax_lane = cfg.chain_kmax;
   {  // enough items to give every lane of the grid one: light pixels' 1000-sample chains were the
@@ -1335,8 +1320,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   hipLaunchKernelGGL(chain_plan_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, d->draw_out, n, d->ch_cnt, m, d->ch_px,
                      d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
-  hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, cfg.order_draws ? d->draw_out : d->lpt_cost, n,
-                     d->ch_cnt, d->ch_k, d->ch_items, d->ch_wave_key);
+  hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
+                     d->ch_wave_key);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
   hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, end, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
@@ -1366,7 +1351,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
-  V.tail_left = cfg.tail_left > 0.0f ? (int32_t)ceilf(cfg.tail_left * (float)V.S.cam.spp) : 0;
   if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
@@ -1800,7 +1784,7 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   HIP_OK(hipMemcpy(sgt.data(), d->seg_time, 3 * n_seg * sizeof(uint32_t), hipMemcpyDeviceToHost));
   const uint32_t spp = (uint32_t)d->view.cam.spp;
   for (size_t k = 0; k < n_items && (int64_t)k < max_rows; k++) {
-    const uint32_t p = items[k].x, sg = items[k].y & ~b1::kItemCrit;
+    const uint32_t p = items[k].x, sg = items[k].y;
     uint32_t *r = rows + 16 * k;
     r[0] = p;
     r[3] = k < c[kCnNCoop] ? 1u : 0u;
