@@ -453,16 +453,24 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
 }
 
 __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk,
-                                                            uint2 *items, uint64_t *wave_key) {
+                                                            uint2 *items, uint64_t *wave_key, int tile_w) {
   // two-level: the block's items per bucket are counted in LDS, one global atomic per bucket and
   // block reserves their range (one global atomic per pixel on 256 bucket words serialised: 3 ms
-  // for a full frame)
+  // for a full frame).  tile_w > 0 (the launch's row width): a block takes a 16 x 16 pixel tile
+  // instead of 256 pixels of a row, so that a bucket's run of items (one block's items of a bucket
+  // are adjacent) comes from one patch of the image
   __shared__ uint32_t cnt_l[257], base_l[257];
   const int stride = gridDim.x * blockDim.x;
-  for (int p0 = blockIdx.x * blockDim.x; p0 < n; p0 += stride) {
+  const int tpr = tile_w > 0 ? (tile_w + 15) / 16 : 0, rows = tile_w > 0 ? n / tile_w : 0;
+  const int span = tile_w > 0 ? tpr * ((rows + 15) / 16) * 256 : n;
+  for (int p0 = blockIdx.x * blockDim.x; p0 < span; p0 += stride) {
     for (int k = threadIdx.x; k < 257; k += blockDim.x) cnt_l[k] = 0u;
     __syncthreads();
-    const int p = p0 + (int)threadIdx.x;
+    int p = p0 + (int)threadIdx.x;
+    if (tile_w > 0) {
+      const int tile = p >> 8, tx = (tile % tpr) * 16 + (p & 15), ty = (tile / tpr) * 16 + ((p >> 4) & 15);
+      p = tx < tile_w && ty < rows ? ty * tile_w + tx : n;
+    }
     uint32_t K = 0u, b = 256u, loc = 0u, cc = 0u;
     if (p < n) {
       K = kk[p] & 0xffffu;
@@ -577,6 +585,7 @@ struct Config {
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
+  bool tile_order = false; // chain items of one cost bucket grouped by 16 x 16 image tiles (chain_scatter_kernel)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -604,6 +613,7 @@ struct Config {
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
+    c.tile_order = env_flag("RT_TILE_ORDER", c.tile_order);
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -1321,7 +1331,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
                      d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
-                     d->ch_wave_key);
+                     d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
   hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, end, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
