@@ -106,7 +106,7 @@ struct MigRec {       // 64 B
 constexpr uint32_t kItemUnsplit = 0x80000000u;  // ch_items[].y: K == 1, the whole pixel
 constexpr uint64_t kEndEnded = 1ull << 63;      // end word: the segment's chain has ended
 constexpr uint64_t kEndNoLink = 1ull << 62;     //   ... without coupling (pixel complete / list full)
-constexpr uint32_t kRecFill = 0xffffffffu;      // ch_end before the record is written
+constexpr uint32_t kRecFill = 0xffffffffu;      // a record's end word (ch_col .w) before the record is written
 constexpr uint32_t kNoTarget = 0xff000000u;     // coupling cursor (t << 24 | c): none
 constexpr int kMaxSeg = 255;                    // t fits 8 bits (host: chain planner caps K lower)
 RT_D uint32_t end_n(uint64_t w) { return (uint32_t)(w >> 32) & 0x3fffffffu; }
@@ -121,6 +121,16 @@ RT_D uint32_t ld_rel(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_R
 RT_D uint64_t ld_rel64(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D void st_rel(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 RT_D void st_rel64(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// One 16-B write-through (sc1) store, the 16-B form of st_rel: the other XCDs' relaxed agent loads
+// (global_load sc1) of any of its words see the stored value (MI355X_MICROARCH.md, visibility: 16-B
+// sc1 stores observed untorn; one fabric write, where a 4-B sc1 store costs ~6x per byte).  The asm
+// ends with s_nop 1 so the next instruction cannot overwrite the data registers before the store reads
+// them.
+RT_D void st_rel128(float4 *p, float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v x = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+}
 RT_D uint32_t ld_acq(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
 
 struct Book1View {
@@ -146,8 +156,7 @@ struct Book1View {
   const uint2 *ch_items;     // {pixel, segment | kItemUnsplit}: whole-wave items first, then lanes'
   const uint32_t *ch_n_items;
   uint64_t *ch_seg;          // segment end words (0: running)
-  float4 *ch_col;            // records: colour, end offset (bits)
-  uint32_t *ch_end;          // records: end offset (kRecFill until written)
+  float4 *ch_col;            // records: colour, end offset (bits; kRecFill until written)
   float4 *ch_acc0;           // per pixel: segment 0's colour sum when it coupled
   uint32_t *seg_time;        // diagnostic (RT_PX_TIME=1): per segment {start, end, migrated} at end0 + k
   const ChainCont *ch_cont;  // continuation launch: items from here (else null)
@@ -168,6 +177,8 @@ struct Book1View {
   uint32_t mig_drop;     // fault injection (tests only): helpers drop this many popped items unrun
   uint64_t mig_wait;     // a helper idle this long (wall_clock64 ticks, 100 MHz) offers to leave
 };
+// a record's end word (ch_col[i].w), read as st_rel128 published it
+RT_D uint32_t rec_end(const Book1View &V, uint32_t i) { return ld_rel((const uint32_t *)&V.ch_col[i] + 3); }
 
 // ---------------------------------------------------------------- chain segments
 RT_D uint32_t seg_start(const ChainPx &P, uint32_t t) { return t * P.seg_len; }
@@ -569,7 +580,7 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_
     if (st > x) return false;  // the successor's next sample starts beyond x
     if (st == x) return true;
     if (c < seg_cap(P, t)) {  // st < x: step over record c
-      const uint32_t e = ld_rel(&V.ch_end[rec_index(P, t, c)]);
+      const uint32_t e = rec_end(V, rec_index(P, t, c));
       if (e != kRecFill) {
         st = e;
         tc = (tc & ~kCurRec) | (c + 1u);
@@ -590,7 +601,7 @@ RT_D bool chain_couple(const Book1View &V, const ChainPx &P, uint32_t k, uint32_
     }
     uint32_t s2 = seg_start(P, t2);
     if (c2 > 0) {
-      s2 = ld_rel(&V.ch_end[rec_index(P, t2, c2 - 1u)]);
+      s2 = rec_end(V, rec_index(P, t2, c2 - 1u));
       if (s2 == kRecFill) return false;
     }
     tc = (t2 << 24) | c2;
@@ -675,12 +686,12 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
   return false;
 }
 
-// Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it).
+// Record of a segment >= 1 chain: the sample's colour and end offset (g.n after it), one 16-B
+// write-through store (the coupling scans of other chains read its end word while the launch runs,
+// the fold its colour after it).
 RT_D void chain_record(const Book1View &V, int64_t pix, uint32_t k, uint32_t c, f3 col, uint32_t x_end) {
   const ChainPx &P = V.ch_px[pix];
-  const uint32_t at = rec_index(P, k, c);
-  V.ch_col[at] = make_float4(col.x, col.y, col.z, u2f(x_end));
-  st_rel(&V.ch_end[at], x_end);
+  st_rel128(&V.ch_col[rec_index(P, k, c)], make_float4(col.x, col.y, col.z, u2f(x_end)));
 }
 
 // A chain's start: stream position, and its coupling cursor on its successor.
@@ -1292,7 +1303,7 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     acc = mk(a0.x, a0.y, a0.z);
     total = end_n(w);
     t = end_t(w), c = end_c(w);
-    o = c == 0 ? seg_start(P, t) : V.ch_end[rec_index(P, t, c - 1u)];
+    o = c == 0 ? seg_start(P, t) : __float_as_uint(V.ch_col[rec_index(P, t, c - 1u)].w);
   }
   while (linked && total < spp) {
     if (t == 0 || t >= P.K) break;  // (never: links point forward)

@@ -273,9 +273,31 @@ __global__ void lpt_scan_kernel(uint32_t *hist) {
   }
 }
 
-__global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
+// Image tiles for the scatters' visiting order: index q of a tile-ordered sweep -> the pixel (n = none).
+// Tiles of tw x (256 / tw) pixels (tw a power of two <= 256), row-major; tile_w = 0: q itself.  The
+// items of one cost bucket that one block (or wave) adds are adjacent in the order, so they come from
+// one patch of the image and their rays share BVH nodes (same-box A/B).
+struct TileSweep {
+  int n, tile_w, tw, th, tpr, rows, span;
+  RT_D TileSweep(int n_, int tile_w_, int tw_) : n(n_), tile_w(tile_w_), tw(tw_) {
+    th = 256 / tw;
+    tpr = tile_w > 0 ? (tile_w + tw - 1) / tw : 0;
+    rows = tile_w > 0 ? n / tile_w : 0;
+    span = tile_w > 0 ? tpr * ((rows + th - 1) / th) * 256 : n;
+  }
+  RT_D int pixel(int q) const {
+    if (tile_w <= 0) return q < n ? q : n;
+    const int tile = q >> 8, r = q & 255, tx = (tile % tpr) * tw + r % tw, ty = (tile / tpr) * th + r / tw;
+    return tx < tile_w && ty < rows ? ty * tile_w + tx : n;
+  }
+};
+
+__global__ void lpt_scatter_kernel(const uint32_t *cost, int n, uint32_t *hist, int32_t *order, int tile_w, int tw) {
+  const TileSweep T(n, tile_w, tw);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < T.span; q += gridDim.x * blockDim.x) {
+    const int i = T.pixel(q);
+    if (i < n) order[atomicAdd(&hist[256 + lpt_bucket(cost[i])], 1u)] = i;
+  }
 }
 
 // Bitonic sort (descending) in LDS, one workgroup: the chain planner's whole-wave items exactly
@@ -453,24 +475,18 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
 }
 
 __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk,
-                                                            uint2 *items, uint64_t *wave_key, int tile_w) {
+                                                            uint2 *items, uint64_t *wave_key, int tile_w, int tw) {
   // two-level: the block's items per bucket are counted in LDS, one global atomic per bucket and
   // block reserves their range (one global atomic per pixel on 256 bucket words serialised: 3 ms
-  // for a full frame).  tile_w > 0 (the launch's row width): a block takes a 16 x 16 pixel tile
-  // instead of 256 pixels of a row, so that a bucket's run of items (one block's items of a bucket
-  // are adjacent) comes from one patch of the image
+  // for a full frame).  tile_w > 0 (the launch's row width): a block takes an image tile
+  // (TileSweep) instead of 256 pixels of a row
   __shared__ uint32_t cnt_l[257], base_l[257];
   const int stride = gridDim.x * blockDim.x;
-  const int tpr = tile_w > 0 ? (tile_w + 15) / 16 : 0, rows = tile_w > 0 ? n / tile_w : 0;
-  const int span = tile_w > 0 ? tpr * ((rows + 15) / 16) * 256 : n;
-  for (int p0 = blockIdx.x * blockDim.x; p0 < span; p0 += stride) {
+  const TileSweep T(n, tile_w, tw);
+  for (int p0 = blockIdx.x * blockDim.x; p0 < T.span; p0 += stride) {
     for (int k = threadIdx.x; k < 257; k += blockDim.x) cnt_l[k] = 0u;
     __syncthreads();
-    int p = p0 + (int)threadIdx.x;
-    if (tile_w > 0) {
-      const int tile = p >> 8, tx = (tile % tpr) * 16 + (p & 15), ty = (tile / tpr) * 16 + ((p >> 4) & 15);
-      p = tx < tile_w && ty < rows ? ty * tile_w + tx : n;
-    }
+    const int p = T.pixel(p0 + (int)threadIdx.x);
     uint32_t K = 0u, b = 256u, loc = 0u, cc = 0u;
     if (p < n) {
       K = kk[p] & 0xffffu;
@@ -511,17 +527,13 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
   for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = make_uint2((uint32_t)(val[i] >> 32), (uint32_t)val[i]);
 }
 
-// ch_end = kRecFill for the planned records; cnt[kCnFilled] = the end of the filled range.
-__global__ void chain_fill_kernel(uint32_t *cnt, uint32_t *ch_end, uint32_t cap) {
+// every planned record's end word = kRecFill; cnt[kCnFilled] = the end of the filled range.
+__global__ void chain_fill_kernel(uint32_t *cnt, float4 *ch_col, uint32_t cap) {
   const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kCnFilled] = n;
-  const uint32_t n4 = n / 4;
-  uint4 *e4 = (uint4 *)ch_end;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x)
-    e4[i] = make_uint4(b1::kRecFill, b1::kRecFill, b1::kRecFill, b1::kRecFill);
-  for (uint32_t i = 4 * n4 + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    ch_end[i] = b1::kRecFill;
+  const float4 fill = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(b1::kRecFill));
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ch_col[i] = fill;
 }
 
 constexpr size_t kCounterBytes = 128 + b1::kMigWords * sizeof(uint32_t);  // work counter line + migration words
@@ -585,7 +597,7 @@ struct Config {
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
-  bool tile_order = false; // chain items of one cost bucket grouped by 16 x 16 image tiles (chain_scatter_kernel)
+  int tile_order = 32;      // > 0: chain items of one cost bucket grouped by image tiles this wide, 256 / it high (chain_scatter_kernel)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
                               //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
@@ -613,7 +625,9 @@ struct Config {
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
-    c.tile_order = env_flag("RT_TILE_ORDER", c.tile_order);
+    c.tile_order = env_int("RT_TILE_ORDER", c.tile_order);
+    if (c.tile_order == 1) c.tile_order = 16;
+    if (c.tile_order < 0 || c.tile_order > 256 || (c.tile_order & (c.tile_order - 1))) c.tile_order = 0;
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
     c.book1 = env_flag("RT_BOOK1", true);
     c.book1_lds = env_flag("RT_BOOK1_LDS", true);
@@ -1255,14 +1269,14 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp) {
   const double seg_recs = fmin((double)cfg.chain_margin * spp / 2.0, (double)spp) + cfg.chain_slack;
   const size_t per_px = (size_t)ceil((double)(kmax - 1) * seg_recs) + (size_t)spp + (size_t)cfg.chain_slack;
   size_t want = npix * per_px;
-  const size_t budget = cfg.chain_mb * ((size_t)1 << 20) / (sizeof(float4) + sizeof(uint32_t));
+  const size_t budget = cfg.chain_mb * ((size_t)1 << 20) / sizeof(float4);
   if (want > budget) want = budget;
   if (want > 0xfff00000u) want = 0xfff00000u;  // u32 record indices
   if (want <= d->ch_rec_cap) return 0;
   if (d->ch_rec_arena) HIP_OK(hipFree(d->ch_rec_arena));
   d->ch_rec_arena = nullptr;
   d->ch_rec_cap = 0;
-  HIP_OK(hipMalloc(&d->ch_rec_arena, want * (sizeof(float4) + sizeof(uint32_t)) + 256));
+  HIP_OK(hipMalloc(&d->ch_rec_arena, want * sizeof(float4) + 256));
   d->ch_rec_cap = want;
   return 0;
 }
@@ -1325,15 +1339,14 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.rec_cap = (uint32_t)d->ch_rec_cap;
   m.seg_cap = d->ch_seg_cap;
   float4 *col = (float4 *)d->ch_rec_arena;
-  uint32_t *end = (uint32_t *)(col + d->ch_rec_cap);
   hipLaunchKernelGGL(chain_params_kernel, dim3(1), dim3(64), 0, st, sums, d->ch_cnt, m);
   hipLaunchKernelGGL(chain_plan_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, d->draw_out, n, d->ch_cnt, m, d->ch_px,
                      d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
-                     d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0);
+                     d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
-  hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, end, (uint32_t)d->ch_rec_cap);
+  hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, col, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
   if (cfg.debug) {  // diagnostic: synchronous peek at the plan
     uint32_t c[16];
@@ -1348,7 +1361,6 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.ch_n_items = d->ch_cnt + kCnItems;
   V.ch_seg = d->ch_seg;
   V.ch_col = col;
-  V.ch_end = end;
   V.ch_acc0 = d->ch_acc0;
   V.ch_cont = nullptr;
   V.ch_n_cont = nullptr;
@@ -1557,7 +1569,8 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       const int n = (int)npix, nb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
       hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, st, d->lpt_hist);
-      hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order);
+      hipLaunchKernelGGL(lpt_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, d->lpt_order,
+                         cfg.tile_order ? G.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16);
       HIP_OK(hipGetLastError());
       G.order = d->lpt_order;
     }

@@ -43,9 +43,13 @@ step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_AC
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- python3 bench.py $A
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write -o run -- python3 bench.py $A
 # the L2's atomics and its memory-side requests (the chain protocol's cross-XCD words; box-to-box comparison)
-step pmc_atom 600 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum \
-    --output-format csv -d gpurun_out/${TAG}_pmc_atom -o run -- python3 bench.py $A
+# (not fatal: the summary is written without it if this pass fails)
+ATOM=""
+timeout -k 10 -s KILL 600 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum \
+    --output-format csv -d gpurun_out/${TAG}_pmc_atom -o run -- python3 bench.py $A > gpurun_out/${TAG}_pmc_atom.log 2>&1 \
+  && ATOM=gpurun_out/${TAG}_pmc_atom
+echo "== pmc_atom ${ATOM:-failed}"
 python3 scripts/pmc_summary.py gpurun_out/${TAG}_pmc_${KEY}.json --build-id "$BID" --config "$KEY" --samples-per-frame "$SAMPLES" --box "$BOX" \
     --stats gpurun_out/${TAG}_stats --stats-frames 3 --pmc-frames 1 \
-    gpurun_out/${TAG}_pmc_sq1 gpurun_out/${TAG}_pmc_sq2 gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write gpurun_out/${TAG}_pmc_atom
+    gpurun_out/${TAG}_pmc_sq1 gpurun_out/${TAG}_pmc_sq2 gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write $ATOM
 find gpurun_out/${TAG}_stats -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats_${KEY}.csv \;
