@@ -515,14 +515,66 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const CoopRay &C,
 // item; host: book1_upload).  bf_candidate returns false (undecided: a NaN root) or the candidate
 // (r*, p*), p* = -1 for a miss; bf_verify is the ancestor check of a candidate p* >= 0.
 constexpr int kBfSlots = 8;  // 64 x 8 = 512 leaves at most (host-checked)
+#ifndef RT_BF_UNROLL
+#define RT_BF_UNROLL 2
+#endif
+#ifndef RT_BV_UNROLL
+#define RT_BV_UNROLL 1
+#endif
 
-RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
-                       int &out_bp) {
+// The lane's leaves of bf_candidate (slot k: leaf k * 64 + lane), read once per work item: their item
+// positions (RT_BF_POS=1) or their sphere words too (RT_BF_POS=2), so a ray's candidate search needs
+// no dependent LDS round trip per slot
+#ifndef RT_BF_POS
+#define RT_BF_POS 0
+#endif
+struct BfLeaves {
+#if RT_BF_POS >= 1
+  int pos[kBfSlots];
+#endif
+#if RT_BF_POS >= 2
+  float4 q0[kBfSlots];
+#endif
+};
+RT_D void bf_load(const Book1View &V, const float4 *items, BfLeaves &L) {
+#if RT_BF_POS >= 1
   const int lane = __lane_id();
+#pragma unroll
+  for (int k = 0; k < kBfSlots; k++) {
+    const int n = k * 64 + lane;
+    const bool live = n < V.n_bf_leaves;
+    const float4 h = it_q1(items, V.n_items9_alloc, live ? n : 0);
+    const uint32_t hw = __float_as_uint(h.w);
+    L.pos[k] = live ? (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw) : -1;
+#if RT_BF_POS >= 2
+    L.q0[k] = it_q0(items, live ? L.pos[k] : 0);
+#endif
+  }
+#endif
+}
+
+RT_D bool bf_candidate(const Book1View &V, const float4 *items, const BfLeaves &L, const CoopRay &C, float tmin,
+                       float &out_best, int &out_bp) {
   float best = __builtin_inff();
   int bp = 0x7fffffff;  // item position of the best leaf (preorder rank)
   bool nan = false;
-#pragma unroll 2
+#if RT_BF_POS >= 1
+#pragma unroll
+  for (int k = 0; k < kBfSlots; k++) {
+    if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
+    const int pos = L.pos[k];
+    const bool live = pos >= 0;
+#if RT_BF_POS >= 2
+    const float r = coop_sphere_root(L.q0[k], C, tmin);
+#else
+    const float r = coop_sphere_root(it_q0(items, live ? pos : 0), C, tmin);
+#endif
+    nan |= live && r != r;
+    if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
+  }
+#else
+  const int lane = __lane_id();
+#pragma unroll RT_BF_UNROLL
   for (int k = 0; k < kBfSlots; k++) {
     if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
     const int n = k * 64 + lane;
@@ -534,6 +586,7 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C
     nan |= live && r != r;
     if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
   }
+#endif
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {  // argmin over (root, preorder position)
     const float ob = __shfl_xor(best, off);
@@ -550,6 +603,7 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C
 RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, float best, int bp) {
   const int lane = __lane_id();
   bool bad = false;
+#pragma unroll RT_BV_UNROLL
   for (int base = 0; base < bp; base += 64) {  // wave-uniform bound
     const int q = base + lane;
     if (q < bp) {
@@ -732,6 +786,8 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     chain_start(V, (uint32_t)pix, seg, g, tc, st);
   }
   const bool use_bf = V.n_bf_leaves > 0;
+  BfLeaves bfl;
+  if (use_bf) bf_load(V, items9, bfl);
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
   if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
   for (;;) {
@@ -772,7 +828,7 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       C.ra = recip_core(C.a);
       float tmax = __builtin_inff();
       int bp = -1;
-      bool decided = use_bf && bf_candidate(V, items9, C, tmin, tmax, bp);
+      bool decided = use_bf && bf_candidate(V, items9, bfl, C, tmin, tmax, bp);
       // the hit sphere (center, 1/r, material) from its LDS item, and its material's load issued
       // before the ancestor check so that its latency overlaps it
       float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
@@ -858,11 +914,39 @@ RT_D bool mig_push(const Book1View &V, uint32_t m, int32_t pix, uint32_t seg, ui
   return true;
 }
 
+// The scene items of the whole-wave traces in the (not inlined) helper functions: a pointer derived
+// from the LDS symbol itself, so that their loads compile to ds_read (a pointer passed in as a
+// parameter is generic there: flat loads, which wait on both the memory and the LDS counters).
+template <bool kLds>
+__device__ __forceinline__ const float4 *items9_of(const Book1View &V) {
+  extern __shared__ __attribute__((aligned(16))) char rt_items_lds[];
+  return kLds ? (const float4 *)rt_items_lds : (const float4 *)V.items9_g;
+}
+// The launch's view in the helper functions: the kernel argument segment's address, passed as a
+// constant-address-space pointer (a generic reference would make every field read a flat load
+// instead of a scalar one; a callee's own __builtin_amdgcn_kernarg_segment_ptr() is null).
+typedef const __attribute__((address_space(4))) Book1View *KernargView;
+__device__ __forceinline__ KernargView kernarg_view() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (KernargView)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  return nullptr;
+#endif
+}
+// (a pointer argument arrives in VGPRs: made wave-uniform again, the field reads are scalar loads)
+__device__ __forceinline__ const Book1View &view_of(KernargView kv) {
+  const uint64_t a = (uint64_t)kv;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return *(const Book1View *)(KernargView)(((uint64_t)hi << 32) | lo);
+}
+
 // A wave whose lanes have all finished: run the migrated items of its mailbox until every item of
 // the launch is done.
-template <int kMode>
-__device__ __attribute__((noinline)) void mig_help(const Book1View &V, const float4 *items9, uint8_t *__restrict__ out,
-                                                 int64_t total_own) {
+template <int kMode, bool kLds>
+__device__ __attribute__((noinline)) void mig_help(KernargView kv, uint8_t *__restrict__ out, int64_t total_own) {
+  const Book1View &V = view_of(kv);
+  const float4 *items9 = items9_of<kLds>(V);
   const bool l0 = __lane_id() == 0;
   const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) / 64;
   const uint32_t m = wave % kMigBoxes;
@@ -934,8 +1018,10 @@ __device__ __attribute__((noinline)) void mig_help(const Book1View &V, const flo
 
 // A chain launch's whole-wave items (the first *n_coop of ch_items), claimed one per wave through
 // coop_counter by the chain kernel's first *coop_waves_dev waves.  Not inlined (see mig_help).
-__device__ __attribute__((noinline)) void coop_items(const Book1View &V, const float4 *items9,
-                                                   uint8_t *__restrict__ out) {
+template <bool kLds>
+__device__ __attribute__((noinline)) void coop_items(KernargView kv, uint8_t *__restrict__ out) {
+  const Book1View &V = view_of(kv);
+  const float4 *items9 = items9_of<kLds>(V);
   const int64_t n_coop = (int64_t)*V.n_coop;
   for (;;) {
     int k = 0;
@@ -977,12 +1063,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // the chain launch's whole-wave items (heaviest first), in this kernel's first waves: a second
     // kernel next to this one got its CU slots only once workgroups of this one had finished
     // (measured: whole-wave items starting at 64 ms of a 106-ms launch); then on to lane items
-#if defined(__HIP_DEVICE_COMPILE__)
-    const Book1View *Vk = (const Book1View *)__builtin_amdgcn_kernarg_segment_ptr();
-#else
-    const Book1View *Vk = &V;
-#endif
-    coop_items(*Vk, items9, out);
+    coop_items<kLds>(kernarg_view(), out);
   }
   const rt_camera &cam = V.S.cam;
   const f3 du = ld3(cam.delta_u), dv = ld3(cam.delta_v), lf = ld3(cam.origin);
@@ -1273,15 +1354,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   }
 #endif
   if (kMode == kMigMode && V.mig_live > 0) {
-    // (not inlined, so that the whole-wave code does not enlarge the lane loop's register budget;
-    // the view is passed as its kernel argument's address -- V is the kernels' first argument --
-    // because taking V's address would copy it to scratch for the whole kernel)
-#if defined(__HIP_DEVICE_COMPILE__)
-    const Book1View *Vk = (const Book1View *)__builtin_amdgcn_kernarg_segment_ptr();
-#else
-    const Book1View *Vk = &V;
-#endif
-    mig_help<kMode>(*Vk, items9, out, total_own);
+    // (not inlined, so that the whole-wave code does not enlarge the lane loop's register budget; it
+    // reads the view from the kernel argument segment -- V is the kernels' first argument -- because
+    // taking V's address would copy it to scratch for the whole kernel)
+    mig_help<kMode, kLds>(kernarg_view(), out, total_own);
   }
 }
 

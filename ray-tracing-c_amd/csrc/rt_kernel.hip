@@ -355,6 +355,7 @@ struct ChainModel {
   float est_scale;      // stream length estimate x this
   float pad;            // pixels of >= pad_k segments: segments of the planned length over pad x the estimate
   int pad_k;
+  int bucket_shift;     // cost buckets merged 2^this at a time (coarser buckets: longer runs of one image tile)
   uint32_t rec_cap;     // records available
   uint32_t seg_cap;     // end words available
 };
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       atomicAdd(&cnt[kCnWave], (uint32_t)K);
       atomicAdd(&wwork, (unsigned long long)c);
     } else {
-      atomicAdd(&h[lpt_bucket(cc)], (uint32_t)K);
+      atomicAdd(&h[lpt_bucket(cc) >> m.bucket_shift << m.bucket_shift], (uint32_t)K);
     }
   }
   __syncthreads();
@@ -475,7 +476,7 @@ __global__ void chain_scan_kernel(uint32_t *cnt, const unsigned long long *sums,
 }
 
 __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost, int n, uint32_t *cnt, const uint32_t *kk,
-                                                            uint2 *items, uint64_t *wave_key, int tile_w, int tw) {
+                                                            uint2 *items, uint64_t *wave_key, int tile_w, int tw, int bshift) {
   // two-level: the block's items per bucket are counted in LDS, one global atomic per bucket and
   // block reserves their range (one global atomic per pixel on 256 bucket words serialised: 3 ms
   // for a full frame).  tile_w > 0 (the launch's row width): a block takes an image tile
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256) void chain_scatter_kernel(const uint32_t *cost
       K = kk[p] & 0xffffu;
       const bool wave = (kk[p] >> 31) != 0u;
       cc = cost[p] / K;
-      b = wave ? 256u : lpt_bucket(cc);  // 256: the whole-wave list
+      b = wave ? 256u : lpt_bucket(cc) >> bshift << bshift;  // 256: the whole-wave list
       loc = atomicAdd(&cnt_l[b], K);
     }
     __syncthreads();
@@ -597,6 +598,7 @@ struct Config {
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
   int cost_budget = 6000;  // cost pre-pass: traversal steps per pixel before extrapolating (0: none)
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
+  int bucket_shift = 0;     // chain planner cost buckets merged 2^this at a time
   int tile_order = 32;      // > 0: chain items of one cost bucket grouped by image tiles this wide, 256 / it high (chain_scatter_kernel)
   int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
   float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
@@ -626,6 +628,7 @@ struct Config {
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
     c.cost_smooth = env_int("RT_COST_SMOOTH", c.cost_smooth);
     c.tile_order = env_int("RT_TILE_ORDER", c.tile_order);
+    c.bucket_shift = min(max(env_int("RT_BUCKET_SHIFT", c.bucket_shift), 0), 4);
     if (c.tile_order == 1) c.tile_order = 16;
     if (c.tile_order < 0 || c.tile_order > 256 || (c.tile_order & (c.tile_order - 1))) c.tile_order = 0;
     c.cost_smooth = c.cost_smooth < 0 ? 0 : (c.cost_smooth > 64 ? 64 : c.cost_smooth);
@@ -1336,6 +1339,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.kmax_wave = d->b1_lds_bytes ? cfg.chain_kmax_wave : 0;  // no whole waves without the LDS scene
   m.spp = V.S.cam.spp;
   m.min_seg = cfg.chain_min_seg;
+  m.bucket_shift = cfg.bucket_shift;
   m.rec_cap = (uint32_t)d->ch_rec_cap;
   m.seg_cap = d->ch_seg_cap;
   float4 *col = (float4 *)d->ch_rec_arena;
@@ -1344,7 +1348,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
                      d->ch_seg, d->ch_k, d->ch_split);
   hipLaunchKernelGGL(chain_scan_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, sums, m);
   hipLaunchKernelGGL(chain_scatter_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->ch_cnt, d->ch_k, d->ch_items,
-                     d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16);
+                     d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16,
+                     m.bucket_shift);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
   hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, col, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
