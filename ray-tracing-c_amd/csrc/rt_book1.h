@@ -515,66 +515,16 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const CoopRay &C,
 // item; host: book1_upload).  bf_candidate returns false (undecided: a NaN root) or the candidate
 // (r*, p*), p* = -1 for a miss; bf_verify is the ancestor check of a candidate p* >= 0.
 constexpr int kBfSlots = 8;  // 64 x 8 = 512 leaves at most (host-checked)
-#ifndef RT_BF_UNROLL
-#define RT_BF_UNROLL 2
-#endif
-#ifndef RT_BV_UNROLL
-#define RT_BV_UNROLL 1
-#endif
 
-// The lane's leaves of bf_candidate (slot k: leaf k * 64 + lane), read once per work item: their item
-// positions (RT_BF_POS=1) or their sphere words too (RT_BF_POS=2), so a ray's candidate search needs
-// no dependent LDS round trip per slot
-#ifndef RT_BF_POS
-#define RT_BF_POS 0
-#endif
-struct BfLeaves {
-#if RT_BF_POS >= 1
-  int pos[kBfSlots];
-#endif
-#if RT_BF_POS >= 2
-  float4 q0[kBfSlots];
-#endif
-};
-RT_D void bf_load(const Book1View &V, const float4 *items, BfLeaves &L) {
-#if RT_BF_POS >= 1
+RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
+                       int &out_bp) {
   const int lane = __lane_id();
-#pragma unroll
-  for (int k = 0; k < kBfSlots; k++) {
-    const int n = k * 64 + lane;
-    const bool live = n < V.n_bf_leaves;
-    const float4 h = it_q1(items, V.n_items9_alloc, live ? n : 0);
-    const uint32_t hw = __float_as_uint(h.w);
-    L.pos[k] = live ? (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw) : -1;
-#if RT_BF_POS >= 2
-    L.q0[k] = it_q0(items, live ? L.pos[k] : 0);
-#endif
-  }
-#endif
-}
-
-RT_D bool bf_candidate(const Book1View &V, const float4 *items, const BfLeaves &L, const CoopRay &C, float tmin,
-                       float &out_best, int &out_bp) {
   float best = __builtin_inff();
   int bp = 0x7fffffff;  // item position of the best leaf (preorder rank)
   bool nan = false;
-#if RT_BF_POS >= 1
-#pragma unroll
-  for (int k = 0; k < kBfSlots; k++) {
-    if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
-    const int pos = L.pos[k];
-    const bool live = pos >= 0;
-#if RT_BF_POS >= 2
-    const float r = coop_sphere_root(L.q0[k], C, tmin);
-#else
-    const float r = coop_sphere_root(it_q0(items, live ? pos : 0), C, tmin);
-#endif
-    nan |= live && r != r;
-    if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
-  }
-#else
-  const int lane = __lane_id();
-#pragma unroll RT_BF_UNROLL
+  // (unrolled 4 / 8, or the slots' leaf positions or sphere words held in registers per work item:
+  // same N = 1 and N = 8 times, same box, r04)
+#pragma unroll 2
   for (int k = 0; k < kBfSlots; k++) {
     if (k * 64 >= V.n_bf_leaves) break;  // wave-uniform
     const int n = k * 64 + lane;
@@ -586,7 +536,6 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const BfLeaves &
     nan |= live && r != r;
     if (live && r > tmin && r < best) best = r, bp = pos;  // strict: the earlier slot wins ties
   }
-#endif
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {  // argmin over (root, preorder position)
     const float ob = __shfl_xor(best, off);
@@ -603,7 +552,6 @@ RT_D bool bf_candidate(const Book1View &V, const float4 *items, const BfLeaves &
 RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, float best, int bp) {
   const int lane = __lane_id();
   bool bad = false;
-#pragma unroll RT_BV_UNROLL
   for (int base = 0; base < bp; base += 64) {  // wave-uniform bound
     const int q = base + lane;
     if (q < bp) {
@@ -786,8 +734,6 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     chain_start(V, (uint32_t)pix, seg, g, tc, st);
   }
   const bool use_bf = V.n_bf_leaves > 0;
-  BfLeaves bfl;
-  if (use_bf) bf_load(V, items9, bfl);
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
   if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
   for (;;) {
@@ -828,7 +774,7 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       C.ra = recip_core(C.a);
       float tmax = __builtin_inff();
       int bp = -1;
-      bool decided = use_bf && bf_candidate(V, items9, bfl, C, tmin, tmax, bp);
+      bool decided = use_bf && bf_candidate(V, items9, C, tmin, tmax, bp);
       // the hit sphere (center, 1/r, material) from its LDS item, and its material's load issued
       // before the ancestor check so that its latency overlaps it
       float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
