@@ -127,9 +127,14 @@ RT_D void st_rel64(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_
 // ends with s_nop 1 so the next instruction cannot overwrite the data registers before the store reads
 // them.
 RT_D void st_rel128(float4 *p, float4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
   typedef float f4v __attribute__((ext_vector_type(4)));
   const f4v x = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+#else
+  // (the host harnesses: tests/native/chain_sim.cpp runs the protocol single-threaded)
+  *p = v;
+#endif
 }
 RT_D uint32_t ld_acq(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -1325,7 +1330,7 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     acc = mk(a0.x, a0.y, a0.z);
     total = end_n(w);
     t = end_t(w), c = end_c(w);
-    o = c == 0 ? seg_start(P, t) : __float_as_uint(V.ch_col[rec_index(P, t, c - 1u)].w);
+    o = c == 0 ? seg_start(P, t) : f2u(V.ch_col[rec_index(P, t, c - 1u)].w);
   }
   while (linked && total < spp) {
     if (t == 0 || t >= P.K) break;  // (never: links point forward)

@@ -85,7 +85,6 @@ int main(int argc, char **argv) {
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg;
   std::vector<float4> col;
-  std::vector<uint32_t> endw;
   std::vector<float4> acc0(npix);
   std::vector<uint32_t> split;
   std::vector<Chain> chains;
@@ -131,8 +130,7 @@ int main(int argc, char **argv) {
       chains.push_back(c);
     }
   }
-  col.assign(rec, make_float4(0, 0, 0, 0));
-  endw.assign(rec, b1::kRecFill);
+  col.assign(rec, make_float4(0, 0, 0, b1::u2f(b1::kRecFill)));  // (end word kRecFill: chain_fill_kernel)
   std::vector<uint32_t> mig(b1::kMigWords, 0u);
   b1::Book1View V;
   memset(&V, 0, sizeof V);
@@ -140,7 +138,6 @@ int main(int argc, char **argv) {
   V.ch_px = px.data();
   V.ch_seg = seg.data();
   V.ch_col = col.data();
-  V.ch_end = endw.data();
   V.ch_acc0 = acc0.data();
   V.mig = mig.data();
   V.mig_epoch = 1u;
@@ -182,7 +179,7 @@ int main(int argc, char **argv) {
     }
     f3 acc = mk(acc0[p].x, acc0[p].y, acc0[p].z);
     uint32_t total = b1::end_n(w), t = b1::end_t(w), c = b1::end_c(w);
-    uint32_t o = c == 0 ? b1::seg_start(P, t) : endw[b1::rec_index(P, t, c - 1)];
+    uint32_t o = c == 0 ? b1::seg_start(P, t) : b1::f2u(col[b1::rec_index(P, t, c - 1)].w);
     for (;;) {
       if (t == 0 || t >= P.K) {
         fprintf(stderr, "pixel %u: bad link %u\n", p, t);
