@@ -22,7 +22,7 @@ case "${PART:-s1}" in
     CHAIN_ROWS=1 step chain_8_7 300 python -u scripts/chain_probe.py 8 7 1000
     ;;
   s7)
-    TAG=r04 CFG="--scene 7 --width 1000 --spp 1000" bash scripts/gpu_profile.sh || exit $?
+    TAG=r04s7 CFG="--scene 7 --width 1000 --spp 1000" bash scripts/gpu_profile.sh || exit $?
     ;;
   pmc)
     SKIP_BENCH=1 TAG=r04b CFG="--scene 1 --width 1200 --spp 1000" bash scripts/gpu_profile.sh || exit $?
