@@ -580,7 +580,11 @@ struct Config {
   bool lpt = true, bf = true, px_time = false, debug = false;
   int lpt_spp = 16, shade_batch = 48;
   int mode = kModeAuto;
-  float chain_beta = 0.7f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
+  // chain_beta: a lane chain's latency target as a fraction of the launch's throughput time; 0 = by
+  // the launch's occupancy: 0.9 at 5 waves per SIMD (N = 1: fewer splits, same box 244.6-245.2 vs
+  // 246.6-247.8 ms at 0.7, 1.0 mixed), 0.7 at 3 (the shares: N = 4 95.2-96.1 ms at 0.7 vs 98.4-102.5 at
+  // 0.9, N = 8 the same within noise)
+  float chain_beta = 0.0f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
   float chain_pad = 1.2f;  // padded plan (chain_plan_kernel; 1: off) for pixels of >= chain_pad_k segments
@@ -1321,7 +1325,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.lat = kLaneLat;
   m.thr = kLaneThr;
   m.coop = kCoopStep;
-  m.beta = cfg.chain_beta;
+  m.beta = cfg.chain_beta > 0.0f ? cfg.chain_beta : (d->chain_occ == 5 ? 0.9f : 0.7f);
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
   m.width = V.S.cam.width;
