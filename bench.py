@@ -112,6 +112,18 @@ def _cpu_model():
     return None
 
 
+def _spread(step_list, kern_list):
+    """Per-step spread of the timed steps (HIP events on the launch stream; the slowest rank per step at
+    N > 1): min / p50 / max of the step and of its frame kernel, and every step's kernel ms, so that a
+    slow launch inside the timed steps shows in the line."""
+    def q(v):
+        v = sorted(v)
+        return {"min": round(v[0], 3), "p50": round(v[len(v) // 2], 3), "max": round(v[-1], 3),
+                "max_over_min": round(v[-1] / v[0], 4) if v[0] > 0 else None} if v else None
+    return {"step_ms": q(step_list), "kernel_ms": q(kern_list),
+            "kernel_ms_per_step": [round(x, 3) for x in kern_list]}
+
+
 def golden_for(args):
     try:
         man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))
@@ -206,17 +218,21 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     ds.check()  # every work item of every timed launch finished (raises otherwise: no number for a partial frame)
-    step_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / max(args.steps, 1)
+    step_list = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    step_ms = sum(step_list) / max(args.steps, 1)
     # the frame kernel alone (HIP events the library records around it on the same stream; the
-    # step also holds the longest-first cost pre-pass and its sort): the last step's launch
-    kernel_ms = ds.last_launch_ms() if n_rows > 0 else -1.0
-    if kernel_ms <= 0:
-        kernel_ms = step_ms
+    # step also holds the longest-first cost pre-pass and its sort): per timed step, and the last one
+    kern_list = ds.launch_history(args.steps) if n_rows > 0 else []
+    if len(kern_list) != args.steps or min(kern_list, default=-1.0) <= 0:
+        kern_list = list(step_list)
+    kernel_ms = kern_list[-1] if kern_list else step_ms
 
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed, kernel_ms] + step_list + kern_list, dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms_max = t.tolist()
+        v = t.tolist()
+        elapsed, kernel_ms_max = v[0], v[1]
+        step_list, kern_list = v[2:2 + args.steps], v[2 + args.steps:]  # per step: the slowest rank
     else:
         kernel_ms_max = kernel_ms
 
@@ -320,6 +336,7 @@ def main():
                                  "bit-exact code (no contraction). achieved counts algorithmic FP32 ops only; traffic "
                                  "= FETCH_SIZE x 2 + WRITE_SIZE bytes per frame from the committed PMC pass of "
                                  "this build (build_id); pmc 'stale' = the committed pass measured another build"},
+            "spread": _spread(step_list, kern_list),
             "cpu_baseline": base,
             "end_to_end": e2e,
             "parity": parity,

@@ -92,12 +92,18 @@ int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigne
  * (rt_book1_cost_kernel, chain_* planner kernels).  -1 when unavailable. */
 double rt_scene_last_launch_ms(rt_device_scene *dscene);
 
+/* The same for the scene's last min(max, 64) launches, oldest first, into ms[]: returns how many were
+ * written (-1 on error; a launch whose kernels record no bracket, e.g. a deep-path launch, reads -1).
+ * bench.py reports their spread (min / p50 / max per step). */
+int rt_scene_launch_history(rt_device_scene *dscene, double *ms, int max);
+
 /* Diagnostics (RT_PX_TIME=1 set at upload time): the last chain launch, one row of 16 uint32 per work
  * item in item order: pixel, segment, K, whole-wave (1) / lane (0), start, end (wall_clock64 ticks,
  * 100 MHz, low 32 bits), records written (samples for segment 0 / unsplit), flags (bit 0 coupled,
  * bit 1 ended), link segment, link record, segment length (draws), the pixel's pre-pass draws, the
- * pixel's pre-pass cost (traversal steps), the tick at which a helper wave took the item over (tail
- * migration; 0: never migrated), 2 reserved (0).
+ * pixel's own pre-pass cost (traversal steps), the tick at which a helper wave took the item over (tail
+ * migration; 0: never migrated), the planner's cost of the pixel (max(own, row-neighbour mean) when
+ * cost smoothing is on, else the own cost), 1 reserved (0).
  * Returns the number of items (at most max_rows rows are written), -1 on error. */
 int64_t rt_scene_chain_diag(rt_device_scene *dscene, uint32_t *rows, int64_t max_rows);
 

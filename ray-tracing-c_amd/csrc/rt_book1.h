@@ -304,6 +304,15 @@ RT_D void sphere_test_data(float4 s, int idx, Lane &L, float tmin) {
 // (skip = 1 + the node's subtree size in items).  The box test sees exactly the reference's t_max:
 // every item before p in preorder that the reference would test has been tested, in order.
 constexpr uint32_t kLeaf9 = 0x80000000u;
+// Sibling leaves (RT_LEAF_PAIR): a leaf item whose successor in preorder is a leaf too (the two children
+// of an n == 2 node, src/hittable.c:294-299) carries kLeafPair, and the step tests both spheres -- the
+// second at the t_max the first left, as BVHNode_hit does (src/hittable.c:270-276) -- so a lane spends
+// one step on the pair instead of two.  The leaf's sphere index sits in the bits below (kLeafIdx).
+constexpr uint32_t kLeafPair = 0x40000000u, kLeafIdx = 0x3fffffffu;
+#ifndef RT_LEAF_PAIR
+#define RT_LEAF_PAIR 0
+#endif
+constexpr bool kPairLeaves = RT_LEAF_PAIR != 0;
 // Items are stored as two arrays (q0 of every item, then q1 of every item: na = V.n_items9_alloc
 // apart): a ds_read_b128 lane group (16 lanes, one 256-B bank row) then spreads random items over 16
 // slots, where 32-B interleaved items use only 8 of them (more bank conflicts on the step's read).
@@ -331,7 +340,13 @@ RT_D bool trav_step_v9(const float4 *items, uint32_t na16, uint32_t n16, Lane &L
   // the straight-line step measured 1.3x slower)
   uint32_t next = p + 16u;
   if (w & kLeaf9) {
+    f4v u = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (kPairLeaves) u = *(const f4v *)(base + p + 16u);  // the successor's q0 (in bounds: the pad item)
     sphere_test_data(q0, (int)p, L, tmin);  // (the hit is the leaf's item: its q1 holds 1/r and the material)
+    if (kPairLeaves && (w & kLeafPair)) {
+      sphere_test_data(make_float4(u.x, u.y, u.z, u.w), (int)(p + 16u), L, tmin);
+      next = p + 32u;
+    }
   } else {
     if (!aabb_packed(q0, q1, L, tmin)) next = p + (__float_as_uint(q1.z) << 4);
   }
@@ -499,7 +514,7 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const CoopRay &C,
       }
       at -= kStop;  // an accepted sphere: t_max shrinks, the walk goes on after it
       tmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0), at));
-      hit = (int)((uint32_t)__builtin_amdgcn_readlane((int)meta, at) & 0x7fffffffu);
+      hit = (int)((uint32_t)__builtin_amdgcn_readlane((int)meta, at) & kLeafIdx);
       p = base + at + 1;
     }
   }
@@ -1025,7 +1040,9 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   int mode = kWait;
 #ifdef RT_LOOP_STATS
   uint64_t st_cyc[2] = {0, 0}, st_last = 0, st_it[2] = {0, 0}, st_lanes[2] = {0, 0}, st_live = 0;
-  uint64_t st_step[4] = {0, 0, 0, 0};  // wave-steps, their stepping lanes, wave-steps running the sphere block, leaf lanes
+  // wave-steps, their stepping lanes, wave-steps running the sphere block, leaf lanes, leaf lanes at the
+  // first of two sibling leaves (kLeafPair), wave-steps whose leaf lanes are all at such a first leaf
+  uint64_t st_step[6] = {0, 0, 0, 0, 0, 0};
   int st_kind = 0;
 #endif
   bool mig_ok = false;     // migration gate (wave-uniform) and the time of its next check
@@ -1090,12 +1107,18 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           for (int u = 0; u < kSteps; u++) {
 #ifdef RT_LOOP_STATS
             {  // per wave-step: stepping lanes, and whether (and for how many lanes) the sphere block runs
-              bool at_leaf = false;
-              if (mode == kTrav) at_leaf = (__float_as_uint(it_q1(items9, V.n_items9_alloc, L.cur >> 4).w) & kLeaf9) != 0u;
-              const uint64_t stepping = __ballot(mode == kTrav), lm = __ballot(at_leaf);
+              bool at_leaf = false, at_pair = false;
+              if (mode == kTrav) {
+                const uint32_t hw = __float_as_uint(it_q1(items9, V.n_items9_alloc, L.cur >> 4).w);
+                at_leaf = (hw & kLeaf9) != 0u;
+                at_pair = at_leaf && (hw & kLeafPair) != 0u;
+              }
+              const uint64_t stepping = __ballot(mode == kTrav), lm = __ballot(at_leaf), pm = __ballot(at_pair);
               if (stepping) {
                 st_step[0]++, st_step[1] += (uint32_t)__popcll(stepping);
                 if (lm) st_step[2]++, st_step[3] += (uint32_t)__popcll(lm);
+                st_step[4] += (uint32_t)__popcll(pm);
+                if (lm && lm == pm) st_step[5]++;
               }
             }
 #endif
@@ -1301,7 +1324,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     atomicAdd(o + 5, (unsigned long long)st_cyc[1]);
     atomicAdd(o + 6, (unsigned long long)st_live);
     if (kMode == 2)
-      for (int q = 0; q < 4; q++) atomicAdd(V.loop_stats + 24 + q, (unsigned long long)st_step[q]);
+      for (int q = 0; q < 6; q++) atomicAdd(V.loop_stats + 24 + q, (unsigned long long)st_step[q]);
   }
 #endif
   if (kMode == kMigMode && V.mig_live > 0) {

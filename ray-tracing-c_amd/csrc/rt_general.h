@@ -157,6 +157,96 @@ RT_D f3 xs_pop(XStack<kN> &S, const float4 *spill) {
   }
 }
 
+// ---- a path's record: what Camera_ray_color's recursion keeps on its stack (src/raytracing.c:39-75)
+// per scattered bounce k: the albedo a_k and, on the light-mixture branch, the pdf weight w_k; the fold
+// computes c = 0 + (a_k (x) c) * w_k innermost first from the path's tail, as the recursion returns
+// (src/raytracing.c:57, :69-71).  Albedos as run-length codes (PathRuns) or on the explicit stack
+// (XStack); weights on the weight stack (RegStack), except a weight of exactly 2.0f -- sp / (0.5f sp)
+// for a direction that misses every light (lights_pdf 0 at light_prob 0.5), 47 % of scene 7's
+// weights -- which is one bit of w2 (bounce index k < kMaxDepth = 64) and takes no stack slot.
+// tests/native/stack_check.cpp checks push and fold against a plain array fold at every stack depth.
+template <int kW, int kX>
+struct PathRecord {
+  PathRuns runs;
+  RegStack<kW> wst;
+  XStack<kX> xst;
+  uint64_t w2;      // bit k: bounce k's weight is 2.0f
+  uint32_t nonfin;  // channels (bit c: channel c) a non-finite record value poisons; a weight: all three
+  int n;            // bounces recorded
+};
+template <int kW, int kX>
+RT_D void rec_init(PathRecord<kW, kX> &P, int albedo_bits) {
+  P.runs = runs_init(albedo_bits);
+#pragma unroll
+  for (int k = 0; k < (kW > 0 ? kW : 1); k++) P.wst.v[k] = 1.0f;
+#pragma unroll
+  for (int k = 0; k < (kX > 0 ? kX : 1); k++) P.xst.v[k] = mk(0.0f, 0.0f, 0.0f);
+  P.wst.n = P.xst.n = 0;
+  P.w2 = 0;
+  P.nonfin = 0;
+  P.n = 0;
+}
+template <int kW, int kX>
+RT_D void rec_clear(PathRecord<kW, kX> &P) {  // a new sample
+  P.runs.w = 0;
+  P.wst.n = P.xst.n = 0;
+  P.w2 = 0;
+  P.nonfin = 0;
+  P.n = 0;
+}
+// Bounce P.n: `code` is its albedo code (PathRuns: a solid texture's, the unit albedo's, or explicit),
+// plus the weighted bit when it has a pdf weight w (else w is 1.0f and unused).  xrec / xw: the thread's
+// kMaxDepth slots for what leaves the register stacks.
+template <int kW, int kX>
+RT_D void rec_push(PathRecord<kW, kX> &P, uint32_t code, f3 albedo, float w, float4 *xrec, float *xw) {
+  const uint32_t code_explicit = (1u << P.runs.cb) - 1u, code_weighted = 1u << P.runs.cb;
+  if (!runs_push(P.runs, code)) code = code_explicit | code_weighted;  // past the runs: explicit, weighted
+  if ((code & code_explicit) == code_explicit) xs_push(P.xst, albedo, xrec);
+  if ((code & code_weighted) && w == 2.0f) P.w2 |= 1ull << P.n;
+  else if (code & code_weighted) rs_push(P.wst, w, xw);
+  P.nonfin |= (uint32_t)!__builtin_isfinite(albedo.x) | ((uint32_t)!__builtin_isfinite(albedo.y) << 1) |
+              ((uint32_t)!__builtin_isfinite(albedo.z) << 2) | (__builtin_isfinite(w) ? 0u : 7u);
+  P.n++;
+}
+// The path's colour from its tail (the last bounce's return value: background, emission, or 0 at the
+// depth cut).  colors: the solid textures' colours by code - 1.
+// Zero tails: when the tail is zero in every channel (a miss into a black background -- scene 7,
+// src/main.c:269 --, the depth cut, src/raytracing.c:40-41, the back face of a light) and every record
+// value is finite, each step maps +-0 to +0, so c = +0 -- returned without the fold and without
+// reloading the records stored beyond the registers (scene 7: 48 % of paths, holding 54 % of those
+// entries).  acc + (+0) == acc bit for bit (acc is never -0: it starts at +0).
+template <int kW, int kX, typename Colors>
+RT_D f3 rec_fold(PathRecord<kW, kX> &P, f3 tail, const Colors &colors, const float4 *xrec, const float *xw) {
+  if (tail.x == 0.0f && tail.y == 0.0f && tail.z == 0.0f && P.nonfin == 0u) return mk(0.0f, 0.0f, 0.0f);
+  const PathRuns &R = P.runs;
+  const uint32_t code_explicit = (1u << R.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << R.cb;
+  f3 c = tail;
+  const uint32_t cnt = (uint32_t)(R.w >> 60);
+  const int nr = cnt == 15u ? R.max_runs : (int)cnt;
+  int covered = 0;  // bounces in the runs; those past them are explicit and weighted
+  for (int r = 0; r < nr; r++) covered += (int)((R.w >> (R.run_bits * r + R.code_bits)) & 63u) + 1;
+  int r = nr - 1, left = 0;  // the run bounce k is in, and its bounces not yet folded
+  uint32_t code = code_explicit | code_weighted;
+  f3 a = mk(1.0f, 1.0f, 1.0f);
+  for (int k = P.n - 1; k >= 0; k--) {
+    if (k < covered) {
+      if (left == 0) {  // enter the next run down
+        code = (uint32_t)(R.w >> (R.run_bits * r)) & R.code_mask;
+        left = (int)((R.w >> (R.run_bits * r + R.code_bits)) & 63u) + 1;
+        r--;
+        const uint32_t ca = code & code_explicit;
+        if (ca != code_explicit) a = ca == code_unit ? mk(1.0f, 1.0f, 1.0f) : colors(ca - 1u);
+      }
+      left--;
+    }
+    if ((code & code_explicit) == code_explicit) a = xs_pop(P.xst, xrec);
+    f3 x = mul(a, c);
+    if (code & code_weighted) x = scale(x, (P.w2 >> k) & 1ull ? 2.0f : rs_pop(P.wst, xw));
+    c = add(mk(0.0f, 0.0f, 0.0f), x);
+  }
+  return c;
+}
+
 // -DRT_GEN_STATS: per-wave cycle and lane counters of the batched loop (wave-uniform, s_memtime)
 enum {
   kGsIterRefill = 0, kGsIterTrace, kGsIterShade,  // cycles of loop iterations by what they ran
@@ -166,8 +256,15 @@ enum {
   kGsCycRecord, kGsCycEmit, kGsCycScatter, kGsCycLights, kGsCycFold,
   kGsMatLam, kGsMatMetal, kGsMatDiel, kGsMatIso, kGsMatEnd,  // shaded lanes by material
   kGsTexSolid, kGsTexChecker, kGsTexImage, kGsTexPerlin,     // shaded lanes by (first) texture kind
-  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite, kGsRecords, kGsExplicit, kGsWeighted, kGsN
+  kGsCycScatterPerlin, kGsPassPerlin, kGsMiss, kGsCycCamera, kGsCycBegin, kGsCycTop, kGsCycClassify, kGsCycCommon, kGsCycRare, kGsRareSteps, kGsCycBounce, kGsCycWrite,
+  // per-lane counters from here on (summed over every lane)
+  kGsRecords, kGsExplicit, kGsWeighted,
+  kGsPaths, kGsPathZero, kGsPathTrunc, kGsPathTruncZero,  // paths with records; zero tail; outgrew the stacks
+  kGsSpillSt, kGsSpillStZero,                             // stack entries beyond the registers (all / zero-tail paths)
+  kGsW2, kGsFoldSkips,                                    // weights == 2.0f; folds skipped (zero tail)
+  kGsN
 };
+constexpr int kGsPerLane = kGsRecords;
 
 // ---- the phased scan: pre_step (rt_device.h) split into a class test and an execution, so that a
 // wave runs the rare, expensive entries -- leaving a transform's subtree, entering one (local_ray +
@@ -520,19 +617,14 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   // reference's vec3_add(emission_color, scatter_color) does.  Records: albedo codes (kCode*) in
   // registers, explicit ones on register stacks spilling to the thread's slots (a lane's records share
   // cache lines, where private arrays interleave every dword across the wave's lanes).
-  PathRuns runs = runs_init(V.code_bits);
-  const uint32_t code_explicit = (1u << runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << runs.cb;
-  // (explicit albedos and weights in register stacks, RegStack / XStack; their overflow in the thread's
-  // kMaxDepth global slots)
+  // (PathRecord: albedo codes in a register pair, explicit albedos and weights on register stacks whose
+  // overflow goes to the thread's kMaxDepth global slots)
+  PathRecord<kWReg, kXReg> P;
+  rec_init(P, V.code_bits);
+  const uint32_t code_explicit = (1u << P.runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << P.runs.cb;
   const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
-  RegStack<kWReg> wst;
-  XStack<kXReg> xst;
-#pragma unroll
-  for (int k = 0; k < (kWReg > 0 ? kWReg : 1); k++) wst.v[k] = 1.0f;
-#pragma unroll
-  for (int k = 0; k < (kXReg > 0 ? kXReg : 1); k++) xst.v[k] = mk(0.0f, 0.0f, 0.0f);
-  wst.n = 0, xst.n = 0;
-  int n = 0, depth = 0, s = 0, i = 0, j = 0;
+  const auto solid_color = [&](uint32_t t) { return ld3(S.textures[t].color); };
+  int depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
   uint32_t rays = 0;
   Pcg32 g;
@@ -700,9 +792,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       }
       d = add(add(add(pixel_pos, scale(du, px)), scale(dv, py)), neg(o));
       depth = S.cam.max_depth;
-      n = 0;
-      runs.w = 0;
-      wst.n = 0, xst.n = 0;
+      rec_clear(P);
       need_sample = false;
     }
     GS_ADD(kGsCycCamera, GS_NOW() - gs_c);
@@ -786,13 +876,10 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
               GS_ADD(kGsCycLights, GS_NOW() - gs_c);
             }
           }
-          if (!runs_push(runs, code)) code = code_explicit | code_weighted;
-          if ((code & code_explicit) == code_explicit) xs_push(xst, albedo, V.xrec + rec0);
-          if (code & code_weighted) rs_push(wst, w, V.xw + rec0);
           GS_ADD(kGsRecords, 1);  // (per lane: summed over every lane at the end)
-          GS_ADD(kGsExplicit, (code & code_explicit) == code_explicit);
           GS_ADD(kGsWeighted, (code & code_weighted) != 0);
-          n++;
+          GS_ADD(kGsW2, (code & code_weighted) != 0 && w == 2.0f);
+          rec_push(P, code, albedo, w, V.xrec + rec0, V.xw + rec0);
           o = r.p;
           d = dir;
           depth--;
@@ -809,32 +896,21 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     gs_c = GS_NOW();
     if (!write) {
     // ---- fold innermost-first, accumulate, next sample / pixel (src/raytracing.c:124-131)
-    f3 c = tail;
-    {
-      const uint32_t cnt = (uint32_t)(runs.w >> 60);
-      const int nr = cnt == 15u ? runs.max_runs : (int)cnt;
-      int covered = 0;  // bounces in the runs; those past them are explicit and weighted
-      for (int r = 0; r < nr; r++) covered += (int)((runs.w >> (runs.run_bits * r + runs.code_bits)) & 63u) + 1;
-      int r = nr - 1, left = 0;  // the run bounce k is in, and its bounces not yet folded
-      uint32_t code = code_explicit | code_weighted;
-      f3 a = mk(1.0f, 1.0f, 1.0f);
-      for (int k = n - 1; k >= 0; k--) {
-        if (k < covered) {
-          if (left == 0) {  // enter the next run down
-            code = (uint32_t)(runs.w >> (runs.run_bits * r)) & runs.code_mask;
-            left = (int)((runs.w >> (runs.run_bits * r + runs.code_bits)) & 63u) + 1;
-            r--;
-            const uint32_t ca = code & code_explicit;
-            if (ca != code_explicit) a = ca == code_unit ? mk(1.0f, 1.0f, 1.0f) : ld3(S.textures[ca - 1].color);
-          }
-          left--;
-        }
-        if ((code & code_explicit) == code_explicit) a = xs_pop(xst, V.xrec + rec0);
-        f3 x = mul(a, c);
-        if (code & code_weighted) x = scale(x, rs_pop(wst, V.xw + rec0));
-        c = add(mk(0.0f, 0.0f, 0.0f), x);
-      }
+#ifdef RT_GEN_STATS
+    if (P.n > 0) {
+      const bool zero_tail = tail.x == 0.0f && tail.y == 0.0f && tail.z == 0.0f;
+      const int over = max(0, P.wst.n - kWReg) + max(0, P.xst.n - kXReg);
+      GS_ADD(kGsPaths, 1);
+      GS_ADD(kGsPathZero, zero_tail);
+      GS_ADD(kGsPathTrunc, over > 0);
+      GS_ADD(kGsPathTruncZero, over > 0 && zero_tail);
+      GS_ADD(kGsSpillSt, over);
+      GS_ADD(kGsSpillStZero, zero_tail ? over : 0);
+      GS_ADD(kGsFoldSkips, zero_tail && P.nonfin == 0u);
+      GS_ADD(kGsExplicit, P.xst.n);
     }
+#endif
+    const f3 c = rec_fold(P, tail, solid_color, V.xrec + rec0, V.xw + rec0);
     acc = add(acc, c);
     s++;
     GS_ADD(kGsCycFold, GS_NOW() - gs_c);
@@ -860,7 +936,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
 #ifdef RT_GEN_STATS
   if (V.stats)
     for (int q = 0; q < kGsN; q++)
-      if (lane == 0 || q == kGsRecords || q == kGsExplicit || q == kGsWeighted) atomicAdd(V.stats + q, gs[q]);
+      if (lane == 0 || q >= kGsPerLane) atomicAdd(V.stats + q, gs[q]);
 #endif
 #undef GS_NOW
 #undef GS_ADD

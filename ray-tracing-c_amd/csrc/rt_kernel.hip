@@ -282,13 +282,14 @@ struct TileSweep {
   RT_D TileSweep(int n_, int tile_w_, int tw_) : n(n_), tile_w(tile_w_), tw(tw_) {
     th = 256 / tw;
     tpr = tile_w > 0 ? (tile_w + tw - 1) / tw : 0;
-    rows = tile_w > 0 ? n / tile_w : 0;
+    rows = tile_w > 0 ? (n + tile_w - 1) / tile_w : 0;  // (a partial last row: pixel() bounds-checks)
     span = tile_w > 0 ? tpr * ((rows + th - 1) / th) * 256 : n;
   }
   RT_D int pixel(int q) const {
     if (tile_w <= 0) return q < n ? q : n;
     const int tile = q >> 8, r = q & 255, tx = (tile % tpr) * tw + r % tw, ty = (tile / tpr) * th + r / tw;
-    return tx < tile_w && ty < rows ? ty * tile_w + tx : n;
+    const int i = ty * tile_w + tx;
+    return tx < tile_w && ty < rows && i < n ? i : n;
   }
 };
 
@@ -406,8 +407,10 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
     // padded plan: the estimate's error lands on the last segment, K times its share of the stream
     // (DESIGN.md §5), so a pixel of many segments gets more segments of the same length, reaching past
     // the estimate: the true end falls inside one of them, and those past it stop when the pixel is done
-    if (m.pad > 1.0f && K >= m.pad_k) {
-      const int kp = min(min((int)ceilf((float)K * m.pad), max(m.kmax_lane, m.kmax_wave)), max(K, m.spp / m.min_seg));
+    // (a whole-wave pixel's segments stay within kmax_wave; the padded stream keeps the u32 guard)
+    if (m.pad > 1.0f && K >= m.pad_k && est * m.pad * 2.0 < 4294967295.0) {
+      const int kcap = wave ? m.kmax_wave : max(m.kmax_lane, m.kmax_wave);
+      const int kp = max(K, min(min((int)ceilf((float)K * m.pad), kcap), max(K, m.spp / m.min_seg)));
       seg_len = (uint32_t)ceil(est * m.pad / kp);
       K = kp;
     }
@@ -663,6 +666,7 @@ struct Config {
     if (c.chain_smooth < 0) c.chain_smooth = 0;
     c.chain_est = env_float("RT_CHAIN_EST", c.chain_est);
     c.chain_pad = env_float("RT_CHAIN_PAD", c.chain_pad);
+    c.chain_pad = c.chain_pad < 1.0f ? 1.0f : (c.chain_pad > 2.0f ? 2.0f : c.chain_pad);  // (1, 2]: 1 = off
     c.chain_pad_k = env_int("RT_CHAIN_PAD_K", c.chain_pad_k);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
     c.chain_occ_px = env_float("RT_CHAIN_OCC_PX", c.chain_occ_px);
@@ -693,6 +697,10 @@ struct rt_device_scene {
   int features;
   int width, height;
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
+  // the last kLaunchRing launches' brackets (rt_scene_launch_history); ev_main is the current slot's pair
+  static constexpr int kLaunchRing = 64;
+  hipEvent_t ev_ring[kLaunchRing][2] = {};
+  uint64_t n_launches = 0;
   hipEvent_t ev_done = nullptr;                // end of the last launch: the next one waits for it
   bool launched = false;
   uint32_t *status = nullptr;  // device: completion status of the launches (chain_check_kernel)
@@ -890,6 +898,13 @@ static void book1_pack(const rt_flat_scene *s, HostPack &H) {
       items9[at + 1].z = bits_as_float((uint32_t)((items9.size() - at) / 2));
     };
     for (int k = 0; k < root.count; k++) emit(s->list_items[root.first + k]);
+    // sibling leaves (rt_book1.h: kLeafPair): a leaf followed by a leaf in preorder
+    for (size_t k = 0; k + 1 < items9.size() / 2; k++) {
+      uint32_t a, b;
+      memcpy(&a, &items9[2 * k + 1].w, 4);
+      memcpy(&b, &items9[2 * k + 3].w, 4);
+      if ((a & b1::kLeaf9) && (b & b1::kLeaf9)) items9[2 * k + 1].w = bits_as_float(a | b1::kLeafPair);
+    }
     // one zero item past the end: the step reads its successor before knowing it exists
     items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     items9.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -1181,8 +1196,11 @@ static rt_device_scene *upload_packed(const rt_flat_scene *s, const HostPack &H,
     d->view.pre = (const float4 *)d->pre_arena;
     d->view.n_pre = (int32_t)(H.pre.size() / 2);
   }
-  if (hipEventCreate(&d->ev_main[0]) != hipSuccess || hipEventCreate(&d->ev_main[1]) != hipSuccess ||
-      hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess ||
+  bool ev_ok = true;
+  for (auto &pair : d->ev_ring)
+    for (hipEvent_t &e : pair) ev_ok = ev_ok && hipEventCreate(&e) == hipSuccess;
+  d->ev_main[0] = d->ev_ring[0][0], d->ev_main[1] = d->ev_ring[0][1];
+  if (!ev_ok || hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&d->status, 256) != hipSuccess || hipMemset(d->status, 0, 256) != hipSuccess) {
     rt_set_error("event / status word creation failed on device %d", device);
     rt_scene_release(d);
@@ -1237,8 +1255,9 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
   if (d->status) (void)hipFree(d->status);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
-  for (hipEvent_t e : d->ev_main)
-    if (e) (void)hipEventDestroy(e);
+  for (auto &pair : d->ev_ring)
+    for (hipEvent_t e : pair)
+      if (e) (void)hipEventDestroy(e);
   delete d;
 }
 
@@ -1449,6 +1468,9 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
       fprintf(stderr, "[rtc] loop stats (cumulative): wave-steps %llu, stepping lanes/step %.1f; steps running the sphere "
               "block %.1f%%, leaf lanes in those %.2f\n", w[0], w[0] ? (double)w[1] / w[0] : 0.0,
               w[0] ? 100.0 * w[2] / w[0] : 0.0, w[2] ? (double)w[3] / w[2] : 0.0);
+      fprintf(stderr, "[rtc] loop stats (cumulative): leaf lane-steps at the first of two sibling leaves %.1f%%; "
+              "sphere-block steps whose leaf lanes all are %.1f%%\n", w[3] ? 100.0 * w[4] / w[3] : 0.0,
+              w[2] ? 100.0 * w[5] / w[2] : 0.0);
     }
 #endif
 
@@ -1528,9 +1550,14 @@ static void launch_general(const rt_device_scene *d, bool all, dim3 g, dim3 b, h
 static int pick_mode(const rt_device_scene *d, int64_t npix) {
   const Config &cfg = d->cfg;
   const int spp = d->view.cam.spp;
-  // (a pre-pass of at most a quarter of the frame's spp -- or exactly its spp: the diagnostic "exact
-  // stream lengths" plan of scripts/gpu_r04.sh, RT_LPT_SPP = spp)
-  const bool chain_ok = cfg.lpt && (spp >= 4 * cfg.lpt_spp || (cfg.lpt_spp == spp && spp >= 64)) &&
+  // (a pre-pass of at most a quarter of the frame's spp -- or, in the diagnostic build only, exactly its
+  // spp: the "exact stream lengths" plan of scripts/gpu_r04.sh, RT_LPT_SPP = spp)
+#ifdef RT_DIAG
+  const bool exact_plan = cfg.lpt_spp == spp && spp >= 64;
+#else
+  const bool exact_plan = false;
+#endif
+  const bool chain_ok = cfg.lpt && (spp >= 4 * cfg.lpt_spp || exact_plan) &&
                         spp >= 2 * cfg.chain_min_seg && npix >= 4096 && d->view.cam.max_depth >= 1;
   if (cfg.mode == kModeChain) return chain_ok ? kModeChain : kModeLane;
   if (cfg.mode == kModeLane) return kModeLane;
@@ -1604,7 +1631,8 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
           "kind_other", "cyc_record", "cyc_emit", "cyc_scatter", "cyc_lights", "cyc_fold", "mat_lam", "mat_metal",
           "mat_diel", "mat_iso", "mat_end", "tex_solid", "tex_checker", "tex_image", "tex_perlin",
           "cyc_scatter_perlin", "pass_perlin", "miss", "cyc_camera", "cyc_begin", "cyc_top", "cyc_classify",
-          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write", "records", "explicit", "weighted"};
+          "cyc_common", "cyc_rare", "rare_steps", "cyc_bounce", "cyc_write", "records", "explicit", "weighted",
+          "paths", "path_zero", "path_trunc", "path_trunc_zero", "spill_st", "spill_st_zero", "w2", "fold_skips"};
       fprintf(stderr, "[rtc] gen stats:");
       for (int k = 0; k < gen::kGsN; k++) fprintf(stderr, " %s=%llu", names[k], q[k]);
       fprintf(stderr, "\n");
@@ -1645,6 +1673,10 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
   HIP_OK(hipSetDevice(d->device));
   hipStream_t st = (hipStream_t)stream;
   if (d->launched) HIP_OK(hipStreamWaitEvent(st, d->ev_done, 0));
+  {  // this launch's bracket: the next slot of the ring
+    const int slot = (int)(d->n_launches++ % rt_device_scene::kLaunchRing);
+    d->ev_main[0] = d->ev_ring[slot][0], d->ev_main[1] = d->ev_ring[slot][1];
+  }
   const int rc = render_rows(d, row0, row_stride, n_rows, d_out, st);
   HIP_OK(hipEventRecord(d->ev_done, st));
   d->launched = true;
@@ -1794,7 +1826,8 @@ extern "C" int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t se
 // Diagnostics of the last chain launch (RT_PX_TIME=1 at upload): one row of 16 u32 per work item, in
 // item order -- pixel, segment, K, whole-wave (1) or lane (0), start, end (wall_clock64 ticks, low 32
 // bits), records (samples for segment 0 / unsplit), end flags (bit 0 linked, bit 1 ended), link
-// segment, link record, segment length, the pixel's pre-pass draws and cost, 3 reserved (rt_hip.h).
+// segment, link record, segment length, the pixel's pre-pass draws and own cost, the migration tick,
+// the planner's cost, 1 reserved (rt_hip.h).
 // Returns the number of items (rows written: min(items, max_rows)), or -1.
 extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64_t max_rows) {
   if (!d || !d->book1 || !d->px_time || !d->seg_time) return rt_set_error("rt_scene_chain_diag: upload with RT_PX_TIME=1"), -1;
@@ -1806,9 +1839,11 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   std::vector<uint2> items(n_items);
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg(n_seg);
-  std::vector<uint32_t> pt(3 * npix), sgt(3 * n_seg), draws(npix), costs(npix);
+  std::vector<uint32_t> pt(3 * npix), sgt(3 * n_seg), draws(npix), costs(npix), own(npix);
   HIP_OK(hipMemcpy(draws.data(), d->draw_out, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(costs.data(), d->lpt_cost, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  // (cost smoothing on: lpt_cost holds the planner's max(own, row mean); the pixel's own is cost_own)
+  HIP_OK(hipMemcpy(own.data(), d->cost_own ? d->cost_own : d->lpt_cost, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(items.data(), d->ch_items, n_items * sizeof(uint2), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(px.data(), d->ch_px, npix * sizeof(b1::ChainPx), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(seg.data(), d->ch_seg, n_seg * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1822,8 +1857,9 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
     r[3] = k < c[kCnNCoop] ? 1u : 0u;
     r[8] = r[9] = r[10] = 0u;
     r[11] = draws[p];
-    r[12] = costs[p];
-    r[13] = r[14] = r[15] = 0u;
+    r[12] = own[p];
+    r[13] = r[15] = 0u;
+    r[14] = costs[p];
     if (sg & b1::kItemUnsplit) {
       r[1] = 0, r[2] = 1, r[4] = pt[3 * p], r[5] = pt[3 * p + 1], r[6] = spp, r[7] = 2u, r[13] = pt[3 * p + 2];
     } else {
@@ -1876,4 +1912,21 @@ extern "C" double rt_scene_last_launch_ms(rt_device_scene *d) {
   float ms = 0.0f;
   if (hipEventElapsedTime(&ms, d->ev_main[0], d->ev_main[1]) != hipSuccess) return -1.0;
   return (double)ms;
+}
+
+// The frame-kernel milliseconds of this scene's last min(max, launches, 64) launches, oldest first
+// (after they completed); returns how many were written, or -1.
+extern "C" int rt_scene_launch_history(rt_device_scene *d, double *ms, int max) {
+  if (!d || !ms || max < 0) return rt_set_error("rt_scene_launch_history: bad argument"), -1;
+  const int R = rt_device_scene::kLaunchRing;
+  const int n = (int)(d->n_launches < (uint64_t)R ? d->n_launches : (uint64_t)R);
+  const int m = n < max ? n : max;
+  HIP_OK(hipSetDevice(d->device));
+  for (int k = 0; k < m; k++) {
+    const int slot = (int)((d->n_launches - (uint64_t)m + (uint64_t)k) % (uint64_t)R);
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, d->ev_ring[slot][0], d->ev_ring[slot][1]) != hipSuccess) t = -1.0f;
+    ms[k] = (double)t;
+  }
+  return m;
 }

@@ -163,6 +163,8 @@ def lib() -> ctypes.CDLL:
         L.rt_diag_arith.restype = c_int
         L.rt_scene_last_launch_ms.argtypes = [c_void_p]
         L.rt_scene_last_launch_ms.restype = c_double
+        L.rt_scene_launch_history.argtypes = [c_void_p, c_void_p, c_int]
+        L.rt_scene_launch_history.restype = c_int
         L.rt_scene_kernel.argtypes = [c_void_p]
         L.rt_scene_kernel.restype = c_char_p
         L.rt_scene_check.argtypes = [c_void_p]
@@ -300,6 +302,15 @@ class DeviceScene:
     def last_launch_ms(self) -> float:
         """Duration of the last frame launch (excludes the cost pre-pass); call after it completed."""
         return float(self._L.rt_scene_last_launch_ms(self._h))
+
+    def launch_history(self, n: int) -> list:
+        """Frame-kernel milliseconds of the last min(n, 64) launches, oldest first (rt_scene_launch_history;
+        call after they completed)."""
+        buf = (c_double * max(int(n), 1))()
+        m = self._L.rt_scene_launch_history(self._h, buf, int(n))
+        if m < 0:
+            raise RtcError(f"rt_scene_launch_history: {last_error(self._L)}")
+        return [float(buf[k]) for k in range(m)]
 
     @property
     def kernel_name(self) -> str:

@@ -61,4 +61,11 @@ print("shaded lanes: " + " ".join(f"{k} {100.0 * q[k] / tm:.1f}%" for k in ms))
 tx = ["tex_solid", "tex_checker", "tex_image", "tex_perlin"]
 print("textures (lanes): " + " ".join(f"{k[4:]} {q[k]}" for k in tx) +
       f"; shade passes with a perlin lane {100.0 * q['pass_perlin'] / si:.1f}%")
+if "paths" in q:  # path records (rt_general.h: RT_GEN_REPLAY): how paths end, what outgrows the register stacks
+    P = max(q["paths"], 1)
+    print(f"paths with records {q['paths']}: zero tail {100.0 * q['path_zero'] / P:.1f}%; outgrew the register stacks "
+          f"{100.0 * q['path_trunc'] / P:.2f}% (of those zero tail {100.0 * q['path_trunc_zero'] / max(q['path_trunc'], 1):.1f}%); "
+          f"entries beyond the registers {q['spill_st']} ({100.0 * q['spill_st_zero'] / max(q['spill_st'], 1):.1f}% on "
+          f"zero-tail paths); weights == 2.0f {100.0 * q['w2'] / max(q['weighted'], 1):.1f}% of weighted records; "
+          f"folds skipped {100.0 * q['fold_skips'] / P:.1f}%")
 print([x for x in r.stdout.splitlines() if x.startswith("frame_ms")][-1])

@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = os.path.join(ROOT, "oracle", "_ref", "api_worlds_ref")
 OUT = os.path.join(HERE, "api")
 NAMES = ["surface_normal", "hollow_glass", "metal_fuzz_dof", "quads_xform_medium_light_dof", "depth100_mirror",
-         "one_px_wide", "flat_list_120", "bvh_depth100"]
+         "one_px_wide", "flat_list_120", "bvh_depth100", "bvh_1100_global_items_64spp", "bvh_1100_global_items_16spp",
+         "boxes_1000_preorder_past_lds"]
 
 
 def main():

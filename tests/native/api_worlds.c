@@ -14,6 +14,15 @@
  *   5 a 1-pixel-wide image (48 rows) of a BVH world
  *   6 a flat list of 120 spheres (no BVH), Book-1 materials, 64 spp
  *   7 max_depth 100 on a BVH world of Book-1 materials (the fast path's depth limit)
+ * and, for the product library's size-driven fallbacks (VERDICT r04 "what's weak" 6: reached with the
+ * product build and natural inputs, no diagnostic switch):
+ *   8 a 1100-sphere BVH at 64 spp: 2200 preorder items (70 KiB) exceed the 64 KiB a Book-1 workgroup
+ *     stages in LDS, so the chain kernel reads the items from global memory, and with more than 512
+ *     leaves its whole-wave items take the exact scan (coop_trace9) instead of the candidate trace
+ *   9 the same world at 16 spp: the lane kernel on global-memory items
+ *  10 1000 boxes (6000 quads) in a BVH under a sampled light: ~7000 preorder entries (220 KiB) exceed
+ *     one workgroup's 160 KiB of LDS, so the general path runs its 256-thread kernel with the first
+ *     entries in LDS and the rest in global memory
  * usage: api_worlds <id> <out.rgb>     prints "width height" on stdout */
 #include "hittable.h"
 #include "material.h"
@@ -25,6 +34,26 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+
+/* The drop-in library's C ABI (include/rt_hip.h), when this source is linked to it: weak, so the
+ * reference build (which has none of it) links too.  API_WORLDS_KERNEL=1 prints on stderr the frame
+ * kernel the library picks for the world -- the tests check that worlds 8-10 reach their fallbacks. */
+typedef struct rt_flat_scene rt_flat_scene;
+typedef struct rt_device_scene rt_device_scene;
+extern rt_flat_scene *rt_flatten(const Camera *camera, const World *world) __attribute__((weak));
+extern void rt_flat_free(rt_flat_scene *scene) __attribute__((weak));
+extern rt_device_scene *rt_scene_upload(const rt_flat_scene *scene, int device) __attribute__((weak));
+extern void rt_scene_release(rt_device_scene *dscene) __attribute__((weak));
+extern const char *rt_scene_kernel(const rt_device_scene *dscene) __attribute__((weak));
+
+static void report_kernel(const Camera *c, const World *w) {
+  if (!getenv("API_WORLDS_KERNEL") || !rt_flatten || !rt_scene_upload || !rt_scene_kernel) return;
+  rt_flat_scene *flat = rt_flatten(c, w);
+  rt_device_scene *d = flat ? rt_scene_upload(flat, 0) : NULL;
+  fprintf(stderr, "kernel: %s\n", d ? rt_scene_kernel(d) : "(upload failed)");
+  if (d) rt_scene_release(d);
+  if (flat) rt_flat_free(flat);
+}
 
 static void camera_defaults(Camera *c, int width, float aspect, int spp, int depth) {
   c->aspect_ratio = aspect;
@@ -166,9 +195,42 @@ static void world_bvh_depth100(World *w, Camera *c) {
   add(w, Sphere_new(vec3(0.0f, 0.1f, -1.5f), 0.6f, Dielectric_new(1.5f)));
 }
 
+static void world_big_bvh(World *w, Camera *c, int spp) {
+  camera_defaults(c, 96, 16.0f / 9.0f, spp, 50);
+  c->look_from = vec3(0.0f, 1.2f, 3.0f);
+  c->look_to = vec3(0.0f, 0.0f, -2.0f);
+  ground(w);
+  add(w, random_bvh(1100, 31u, 5.0f));
+}
+
+static void world_many_boxes(World *w, Camera *c) {
+  camera_defaults(c, 64, 1.0f, 64, 20);
+  c->background = vec3(0.05f, 0.05f, 0.08f);
+  c->vfov = 45.0f;
+  c->look_from = vec3(0.0f, 7.0f, 9.0f);
+  c->look_to = vec3(0.0f, 0.0f, 0.0f);
+  PCG32 rng;
+  pcg32_seed(&rng, 41u, 9u);
+  Hittable *boxes = HittableList_new(1000);
+  Material *grey = lamb(0.6f, 0.6f, 0.55f), *blue = lamb(0.2f, 0.3f, 0.7f);
+  for (int k = 0; k < 1000; k++) {
+    const float x = pcg32_f32_between(&rng, -6.0f, 6.0f);
+    const float z = pcg32_f32_between(&rng, -6.0f, 6.0f);
+    const float s = pcg32_f32_between(&rng, 0.1f, 0.35f);
+    const float h = pcg32_f32_between(&rng, 0.1f, 1.2f);
+    HittableList_append((HittableList *)boxes, Box_new(vec3(x, 0.0f, z), vec3(x + s, h, z + s), k % 3 ? grey : blue));
+  }
+  add(w, BVHNode_new((HittableList *)boxes, &rng));
+  add(w, Quad_new(vec3(-8.0f, 0.0f, -8.0f), vec3(16.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 16.0f), lamb(0.4f, 0.45f, 0.3f)));
+  Material *light = DiffuseLight_new(Solid_new(vec3(8.0f, 8.0f, 7.0f)));
+  Hittable *panel = Quad_new(vec3(-1.5f, 5.0f, -1.5f), vec3(3.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 3.0f), light);
+  add(w, panel);
+  HittableList_append(&w->lights, panel);
+}
+
 int main(int argc, char **argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s <world 0-7> <out.rgb>\n", argv[0]);
+    fprintf(stderr, "usage: %s <world 0-10> <out.rgb>\n", argv[0]);
     return 2;
   }
   World world;
@@ -183,12 +245,16 @@ int main(int argc, char **argv) {
     case 5: world_one_px_wide(&world, &camera); break;
     case 6: world_flat_list(&world, &camera); break;
     case 7: world_bvh_depth100(&world, &camera); break;
+    case 8: world_big_bvh(&world, &camera, 64); break;
+    case 9: world_big_bvh(&world, &camera, 16); break;
+    case 10: world_many_boxes(&world, &camera); break;
     default: fprintf(stderr, "unknown world\n"); return 2;
   }
   Camera_init(&camera);
   const size_t n = (size_t)camera.img_width * camera.img_height * 3;
   uint8_t *img = malloc(n);
   Camera_render(&camera, &world, img);
+  report_kernel(&camera, &world);
   FILE *f = fopen(argv[2], "wb");
   if (!f || fwrite(img, 1, n, f) != n) {
     fprintf(stderr, "cannot write %s\n", argv[2]);

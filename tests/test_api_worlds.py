@@ -43,13 +43,17 @@ def test_api_worlds_binary_built():
     assert os.access(EXE, os.X_OK), "make -C tests/native"
 
 
-def _render(wid, tmp_path, env=None):
+def _render(wid, tmp_path, env=None, kernel=False):
     out = tmp_path / f"w{wid}.rgb"
     r = subprocess.run([EXE, wid, str(out)], capture_output=True, text=True, timeout=120,
-                       env={**os.environ, **(env or {})})
+                       env={**os.environ, **(env or {}), **({"API_WORLDS_KERNEL": "1"} if kernel else {})})
     assert r.returncode == 0, r.stderr[-2000:]
     w, h = (int(x) for x in r.stdout.split())
-    return np.fromfile(out, np.uint8).reshape(h, w, 3)
+    img = np.fromfile(out, np.uint8).reshape(h, w, 3)
+    if kernel:
+        names = [x.split("kernel: ", 1)[1] for x in r.stderr.splitlines() if x.startswith("kernel: ")]
+        return img, names[-1] if names else None
+    return img
 
 
 def _check(img, ref, what):
@@ -74,3 +78,24 @@ def test_gpu_api_world_matches_reference_build(wid, tmp_path):
 def test_gpu_api_world_book1_variants(wid, env, tmp_path):
     ref, e = golden(wid)
     _check(_render(wid, tmp_path, env), ref, f"world {wid} ({e['name']}) {env}")
+
+
+# The product library's size-driven fallbacks, reached with librtc_amd.so (no diagnostic build, no
+# RT_* switch) through worlds whose size forces them (tests/native/api_worlds.c 8-10): the frame must
+# match the reference build's and the library must have picked the fallback kernel.
+FALLBACKS = {
+    "8": ("rt_book1_chain_kernel<false,", "Book-1 items past 64 KiB: the chain kernel reads them from global memory"),
+    "9": ("rt_book1_kernel<false>", "the lane kernel on global-memory items"),
+    "10": ("rt_general_kernel<511, true>", "a preorder past one workgroup's LDS: the 256-thread general kernel"),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wid", sorted(FALLBACKS, key=int))
+def test_gpu_product_fallback_paths(wid, tmp_path):
+    ref, e = golden(wid)
+    img, kernel = _render(wid, tmp_path, kernel=True)
+    want, what = FALLBACKS[wid]
+    assert kernel is not None and kernel.replace(" ", "").startswith(want.replace(" ", "")), \
+        f"world {wid}: expected {want} ({what}), the library picked {kernel}"
+    _check(img, ref, f"world {wid} ({e['name']}): {what}")

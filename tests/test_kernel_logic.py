@@ -68,3 +68,18 @@ def test_chain_protocol_on_host_matches_oracle(tmp_path, scene, width, spp, seed
     got = np.fromfile(out, np.uint8).reshape(ref.shape)
     bad = (got != ref).any(axis=2)
     assert not bad.any(), f"{bad.sum()} pixels differ; first at {np.argwhere(bad)[0]}; {r.stdout}"
+
+
+STACK = os.path.join(ROOT, "tests", "native", "bin", "stack_check")
+
+
+def test_path_record_on_host_matches_recursion():
+    """The general kernel's path record (rt_general.h: PathRecord -- run-length albedo codes, the
+    explicit-albedo and weight register stacks and their overflow slots, the weight-2.0f bits, the
+    zero-tail shortcut) on the host under ASan at every register-stack depth RT_GEN_WREG / RT_GEN_XREG
+    can select (0/0 through 8/2): random paths of 1-64 bounces with non-finite values mixed in must fold
+    to the recursion's colour bit for bit (the spill indexing is pinned at every depth)."""
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+    r = subprocess.run([STACK, "20000"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert r.stdout.count("paths ok") == 8, r.stdout

@@ -284,6 +284,22 @@ def test_general_path_shipped_variants(manifest, name, env, monkeypatch):
     _check(img, golden_image(e), f"{name} {env}")
 
 
+@pytest.mark.parametrize("env", [{"RT_GEN_PRE": "0"}, {"RT_GEN_BATCH": "0"}, {"RT_GEN_BATCH": "1"}, {"RT_GEN_BATCH": "64"},
+                                 {"RT_GEN_FLAT": "1"}, {"RT_GEN_RARE": "1"}, {"RT_GEN_STEPS": "3"}, {"RT_LPT_SPP": "2"},
+                                 {"RT_LPT_SPP": "2", "RT_LPT": "0"}])
+def test_general_path_diag_switches(manifest, env, monkeypatch):
+    """The diagnostic build's remaining A/B switches of the general kernel: no preorder
+    (stack traversal), unbatched / one-lane / full-wave shading batches, no extra box entries per step,
+    rare actions at once, short trace iterations, the longest-first pre-pass on (2 spp) or off -- each changes only the
+    schedule, so scene 7 must still reproduce the reference frame."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = manifest["renders"]["s7_200x200_8spp_d50"]
+    with rtc.use_diag():
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+    _check(img, golden_image(e), f"s7 {env}")
+
+
 def test_bench_two_rank_launch_reassembles_reference_frame():
     """bench.py's N-rank path (torch.distributed.run, rows j % N, gather, parity) run as 2 ranks on
     this box's GPU(s) (RT_BENCH_SHARE_DEVICE=1: gloo for the reduction and the gather), on the
