@@ -85,6 +85,9 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
 // (DESIGN.md §4.3); with 4 weights and 1 albedo in registers most paths never touch memory, where
 // every record store used to leave L2 for HBM at >= 32 B.  Only static register indices (unrolled
 // shifts): a dynamically indexed private array would live in scratch.
+#ifndef RT_GEN_EXTRA_SL
+#define RT_GEN_EXTRA_SL 0  // pre_common's extra box actions branch-free (A/B variant)
+#endif
 #ifndef RT_GEN_WREG
 #define RT_GEN_WREG 4  // pdf weights in registers (config 5, same box: 8 / 4 / 0 -> 274 / 276 / 271 Msamples/s)
 #endif
@@ -541,6 +544,25 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   // scan): their LDS reads and slab tests overlap the sphere / quad chains above (T.tmax as those
   // left it); any other entry, or leaving a frame, waits for the next step
   // (the first one straight-line, the rest in a loop: the loop's overhead measured costly at one)
+#if RT_GEN_EXTRA_SL
+  // (RT_GEN_EXTRA_SL: the two extra box actions branch-free -- every lane reads an entry, its next one
+  // or, without one, its current one again -- so the step has no divergent branches there: fewer
+  // exec-mask instructions per step, one more LDS read for the lanes that stop)
+  bool more = extra > 0 && next < (uint32_t)S.n_pre && next < T.fend;
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const bool go = more && extra > e && next < (uint32_t)S.n_pre && next < T.fend;
+    const uint32_t q = go ? next : T.p;
+    const float4 r0 = pre[2 * q], r1 = pre[2 * q + 1];
+    const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
+    const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
+    const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
+    const float lo2 = fmaxf(fmaxf(fmaxf(tmin, ix < 0 ? dx : cx), iy < 0 ? dy : cy), iz < 0 ? dz : cz);
+    const float hi2 = fminf(fminf(fminf(T.tmax, ix < 0 ? cx : dx), iy < 0 ? cy : dy), iz < 0 ? cz : dz);
+    more = go && rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) == RT_KIND_BVH;
+    next = more ? (hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1) : next;
+  }
+#else
   bool more = extra > 0 && next < (uint32_t)S.n_pre && next < T.fend;
   if (more) {
     const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
@@ -563,6 +585,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
     more = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, r1.w)) == RT_KIND_BVH;
     if (more) next = hi2 <= lo2 ? __builtin_bit_cast(uint32_t, r1.z) : next + 1;
   }
+#endif
 #pragma unroll 1
   for (int e = 2; more && e < extra && next < (uint32_t)S.n_pre && next < T.fend; e++) {
     const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];

@@ -262,6 +262,8 @@ constexpr size_t kLptHistBytes = 8192;
 // §5): the slowest lane chain's latency and the lanes' aggregate throughput per pre-pass traversal
 // step, and a whole-wave chain's rate.
 constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
+// tail shaping at 3 waves per SIMD (the N >= 2 shares): ChainModel.alpha (0: off)
+constexpr float kTailAlpha3 = 0.0f;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
@@ -338,7 +340,7 @@ __device__ void bitonic_desc(K *key, T *val, int m) {
 enum : int {
   kCnItems = 0, kCnSplit = 1, kCnFilled = 2, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
   kCnCoopWaves = 7, kCnCoopCounter = 8, kCnNCoop = 9, kCnWaveWork = 10 /* u64 */, kCnCstar = 12, kCnCstarW = 13,
-  kCnHist = 256, kCnOff = 512, kCnWords = 1024
+  kCnHist = 256, kCnOff = 512, kCnCstarB = 768 /* per cost bucket: the lane chain target c*_b (f32) */, kCnWords = 1024
 };
 
 struct ChainModel {
@@ -354,6 +356,8 @@ struct ChainModel {
   int min_seg;          // samples per segment at least
   int width, smooth;    // launch row width; draw estimates averaged over +-smooth pixels of the row
   float est_scale;      // stream length estimate x this
+  float alpha, floor;   // tail shaping (alpha > 0): bucket b's chain target min(beta, max(floor, alpha (1 - F_b))) T,
+                        // F_b = the share of the launch's work in costlier buckets (they start before it)
   float pad;            // pixels of >= pad_k segments: segments of the planned length over pad x the estimate
   int pad_k;
   int bucket_shift;     // cost buckets merged 2^this at a time (coarser buckets: longer runs of one image tile)
@@ -369,6 +373,19 @@ __global__ void chain_params_kernel(const unsigned long long *sums, uint32_t *cn
   const float cstar = (float)fmax(1.0, m.beta * total * m.thr / (lanes * m.lat));
   cnt[kCnCstar] = __float_as_uint(cstar);
   cnt[kCnCstarW] = __float_as_uint(cstar * m.lat / m.coop);
+  // tail shaping: items start longest first, so a pixel of bucket b starts after about F_b of the
+  // launch's work and has (1 - F_b) T left -- its lane chains get that much (alpha x), down to floor T
+  double above = 0.0;
+  for (int b = 255; b >= 0; b--) {
+    float c = cstar;
+    if (m.alpha > 0.0f && total > 0.0) {
+      const float f = (float)(above / total);
+      const float t = fminf(m.beta, fmaxf(m.floor, m.alpha * (1.0f - f)));
+      c = (float)fmax(1.0, (double)cstar * t / m.beta);
+    }
+    cnt[kCnCstarB + b] = __float_as_uint(c);
+    above += (double)sums[b];
+  }
 }
 
 __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, const uint32_t *draws, int n,
@@ -381,7 +398,7 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
   __syncthreads();
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     const uint32_t c = cost[p];
-    const float cstar = __uint_as_float(cnt[kCnCstar]), cstar_w = __uint_as_float(cnt[kCnCstarW]);
+    const float cstar = __uint_as_float(cnt[kCnCstarB + lpt_bucket(c)]), cstar_w = __uint_as_float(cnt[kCnCstarW]);
     int K = (int)fminf(ceilf((float)c / cstar), 1e6f);
     bool wave = false;
     if (K > m.kmax_lane && m.kmax_wave > 0) {  // too long for lane chains: whole-wave chains
@@ -587,7 +604,10 @@ struct Config {
   // the launch's occupancy: 0.9 at 5 waves per SIMD (N = 1: fewer splits, same box 244.6-245.2 vs
   // 246.6-247.8 ms at 0.7, 1.0 mixed), 0.7 at 3 (the shares: N = 4 95.2-96.1 ms at 0.7 vs 98.4-102.5 at
   // 0.9, N = 8 the same within noise)
-  float chain_beta = 0.0f, chain_margin = 1e9f;  // margin: records per segment / (spp / K); >= K: spp
+  float chain_beta = 0.0f, chain_margin = 1e9f;
+  // chain_alpha: tail shaping of the plan (ChainModel.alpha; < 0: by occupancy, kTailAlpha3 at 3 waves per
+  // SIMD, off at 5); chain_floor: its smallest lane chain target, a fraction of the throughput time
+  float chain_alpha = -1.0f, chain_floor = 0.1f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
   float chain_pad = 1.2f;  // padded plan (chain_plan_kernel; 1: off) for pixels of >= chain_pad_k segments
@@ -618,6 +638,8 @@ struct Config {
     c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
     if (c.lpt_spp < 1) c.lpt_spp = 1;
     c.chain_beta = env_float("RT_CHAIN_BETA", c.chain_beta);
+    c.chain_alpha = env_float("RT_CHAIN_ALPHA", c.chain_alpha);
+    c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
     c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ);
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
@@ -1345,6 +1367,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.thr = kLaneThr;
   m.coop = kCoopStep;
   m.beta = cfg.chain_beta > 0.0f ? cfg.chain_beta : (d->chain_occ == 5 ? 0.9f : 0.7f);
+  m.alpha = cfg.chain_alpha >= 0.0f ? cfg.chain_alpha : (d->chain_occ == 5 ? 0.0f : kTailAlpha3);
+  m.floor = cfg.chain_floor;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
   m.width = V.S.cam.width;
