@@ -647,6 +647,13 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   const uint32_t code_explicit = (1u << P.runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << P.runs.cb;
   const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
   const auto solid_color = [&](uint32_t t) { return ld3(S.textures[t].color); };
+  // extra box actions per step: RT_GEN_FLAT - 1 in the diagnostic build; the product's 2 at compile time,
+  // so pre_common's loop for further ones -- and its per-step exec-mask bookkeeping -- compiles away
+#ifdef RT_DIAG
+  const int extra_boxes = V.flat - 1;
+#else
+  constexpr int extra_boxes = 2;
+#endif
   int depth = 0, s = 0, i = 0, j = 0;
   int64_t pix = 0;
   uint32_t rays = 0;
@@ -767,7 +774,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             bool fin = false;
             GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, V.flat - 1);
+            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, extra_boxes);
             GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
             gs_c = GS_NOW();
             if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);

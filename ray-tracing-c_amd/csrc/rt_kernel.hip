@@ -719,9 +719,10 @@ struct rt_device_scene {
   int features;
   int width, height;
   hipEvent_t ev_main[2] = {nullptr, nullptr};  // bracket the last frame launch (rt_scene_last_launch_ms)
-  // the last kLaunchRing launches' brackets (rt_scene_launch_history); ev_main is the current slot's pair
+  // the last kLaunchRing launches' brackets as device timestamps (stamp_kernel: wall_clock64, 100 MHz) --
+  // rt_scene_launch_history; one u64 pair per launch in the scene's status allocation, no extra events
   static constexpr int kLaunchRing = 64;
-  hipEvent_t ev_ring[kLaunchRing][2] = {};
+  uint64_t *ts_ring = nullptr;
   uint64_t n_launches = 0;
   hipEvent_t ev_done = nullptr;                // end of the last launch: the next one waits for it
   bool launched = false;
@@ -1218,12 +1219,11 @@ static rt_device_scene *upload_packed(const rt_flat_scene *s, const HostPack &H,
     d->view.pre = (const float4 *)d->pre_arena;
     d->view.n_pre = (int32_t)(H.pre.size() / 2);
   }
-  bool ev_ok = true;
-  for (auto &pair : d->ev_ring)
-    for (hipEvent_t &e : pair) ev_ok = ev_ok && hipEventCreate(&e) == hipSuccess;
-  d->ev_main[0] = d->ev_ring[0][0], d->ev_main[1] = d->ev_ring[0][1];
-  if (!ev_ok || hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(&d->status, 256) != hipSuccess || hipMemset(d->status, 0, 256) != hipSuccess) {
+  // status words (256 B), then the launch timestamp ring
+  const size_t status_bytes = 256 + rt_device_scene::kLaunchRing * 2 * sizeof(uint64_t);
+  if (hipEventCreate(&d->ev_main[0]) != hipSuccess || hipEventCreate(&d->ev_main[1]) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&d->status, status_bytes) != hipSuccess || hipMemset(d->status, 0, status_bytes) != hipSuccess) {
     rt_set_error("event / status word creation failed on device %d", device);
     rt_scene_release(d);
     return NULL;
@@ -1277,9 +1277,8 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
   if (d->status) (void)hipFree(d->status);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
-  for (auto &pair : d->ev_ring)
-    for (hipEvent_t e : pair)
-      if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d->ev_main)
+    if (e) (void)hipEventDestroy(e);
   delete d;
 }
 
@@ -1336,6 +1335,21 @@ static int chain_occupancy(const rt_device_scene *d, int64_t npix) {
   const int occ = d->cfg.chain_occ;
   if (occ == 3 || occ == 5) return occ;
   return (double)npix >= d->cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 3;
+}
+
+// A launch's bracket: the ev_main event (rt_scene_last_launch_ms) and a device timestamp in the
+// scene's ring (rt_scene_launch_history): one thread writes wall_clock64 with a vector store.
+__global__ void stamp_kernel(uint64_t *p) {
+  if (threadIdx.x == 0) *p = (uint64_t)wall_clock64();
+}
+static hipError_t mark_launch(rt_device_scene *d, int which, hipStream_t st) {
+  if (d->ev_main[which]) {
+    const hipError_t e = hipEventRecord(d->ev_main[which], st);
+    if (e != hipSuccess) return e;
+  }
+  if (!d->ts_ring) return hipSuccess;
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, d->ts_ring + which);
+  return hipGetLastError();
 }
 
 static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
@@ -1425,7 +1439,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz
   V.mig_drop = (uint32_t)cfg.mig_drop;
-  if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+  HIP_OK(mark_launch(d, 0, st));
   const bool lds = d->b1_lds_bytes != 0;
   if (!lds) V.n_coop = nullptr;  // (the planner gives no whole-wave items without the LDS scene)
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
@@ -1468,7 +1482,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   if (C.mig_live > 0)
     hipLaunchKernelGGL(chain_check_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)C.mig, C.ch_n_cont,
                        (const uint32_t *)nullptr, d->status);
-  if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+  HIP_OK(mark_launch(d, 1, st));
   if (cfg.debug) {
     HIP_OK(hipEventRecord(dbg_ev[2], st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1535,13 +1549,13 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
 static int launch_lane(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st) {
   const bool lds = d->b1_lds_bytes != 0;
   V.n_coop = nullptr;
-  if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+  HIP_OK(mark_launch(d, 0, st));
   HIP_OK(hipMemsetAsync(V.work_counter, 0, kCounterBytes, st));  // counter + migration words
   const dim3 g1((unsigned)d->b1_grid), blk(b1::kBlock);
   if (lds) hipLaunchKernelGGL((rt_book1_kernel<true>), g1, blk, d->b1_lds_bytes, st, V, d_out);
   else hipLaunchKernelGGL((rt_book1_kernel<false>), g1, blk, 0, st, V, d_out);
   HIP_OK(hipGetLastError());
-  if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+  HIP_OK(mark_launch(d, 1, st));
   return 0;
 }
 
@@ -1641,7 +1655,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     HIP_OK(hipMemsetAsync(gen_stats, 0, gen::kGsN * sizeof(unsigned long long), st));
     G.stats = gen_stats;
 #endif
-    if (d->ev_main[0]) HIP_OK(hipEventRecord(d->ev_main[0], st));
+    HIP_OK(mark_launch(d, 0, st));
     launch_general(d, all, gg, gb, st, G, d_out);
     HIP_OK(hipGetLastError());
 #ifdef RT_GEN_STATS
@@ -1662,7 +1676,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       fprintf(stderr, "\n");
     }
 #endif
-    if (d->ev_main[1]) HIP_OK(hipEventRecord(d->ev_main[1], st));
+    HIP_OK(mark_launch(d, 1, st));
     return 0;
   }
   if (d->deep_rec) {
@@ -1697,10 +1711,9 @@ extern "C" int rt_render_rows_async(rt_device_scene *d, int row0, int row_stride
   HIP_OK(hipSetDevice(d->device));
   hipStream_t st = (hipStream_t)stream;
   if (d->launched) HIP_OK(hipStreamWaitEvent(st, d->ev_done, 0));
-  {  // this launch's bracket: the next slot of the ring
-    const int slot = (int)(d->n_launches++ % rt_device_scene::kLaunchRing);
-    d->ev_main[0] = d->ev_ring[slot][0], d->ev_main[1] = d->ev_ring[slot][1];
-  }
+  // this launch's timestamps go to the next slot of the ring (mark_launch)
+  d->ts_ring = (uint64_t *)((char *)d->status + 256) + 2 * (d->n_launches++ % rt_device_scene::kLaunchRing);
+  HIP_OK(hipMemsetAsync(d->ts_ring, 0, 2 * sizeof(uint64_t), st));  // (a launch without a bracket reads -1)
   const int rc = render_rows(d, row0, row_stride, n_rows, d_out, st);
   HIP_OK(hipEventRecord(d->ev_done, st));
   d->launched = true;
@@ -1939,18 +1952,20 @@ extern "C" double rt_scene_last_launch_ms(rt_device_scene *d) {
 }
 
 // The frame-kernel milliseconds of this scene's last min(max, launches, 64) launches, oldest first
-// (after they completed); returns how many were written, or -1.
+// (after they completed; from the device timestamps of mark_launch); returns how many were written, or -1.
 extern "C" int rt_scene_launch_history(rt_device_scene *d, double *ms, int max) {
   if (!d || !ms || max < 0) return rt_set_error("rt_scene_launch_history: bad argument"), -1;
   const int R = rt_device_scene::kLaunchRing;
   const int n = (int)(d->n_launches < (uint64_t)R ? d->n_launches : (uint64_t)R);
   const int m = n < max ? n : max;
   HIP_OK(hipSetDevice(d->device));
+  if (d->launched) HIP_OK(hipEventSynchronize(d->ev_done));
+  std::vector<uint64_t> ts(2 * R);
+  HIP_OK(hipMemcpy(ts.data(), (char *)d->status + 256, ts.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   for (int k = 0; k < m; k++) {
     const int slot = (int)((d->n_launches - (uint64_t)m + (uint64_t)k) % (uint64_t)R);
-    float t = 0.0f;
-    if (hipEventElapsedTime(&t, d->ev_ring[slot][0], d->ev_ring[slot][1]) != hipSuccess) t = -1.0f;
-    ms[k] = (double)t;
+    const uint64_t a = ts[2 * slot], b = ts[2 * slot + 1];
+    ms[k] = a && b >= a ? (double)(b - a) * 1e-5 : -1.0;  // wall_clock64: 100 MHz
   }
   return m;
 }

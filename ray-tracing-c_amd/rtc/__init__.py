@@ -163,8 +163,9 @@ def lib() -> ctypes.CDLL:
         L.rt_diag_arith.restype = c_int
         L.rt_scene_last_launch_ms.argtypes = [c_void_p]
         L.rt_scene_last_launch_ms.restype = c_double
-        L.rt_scene_launch_history.argtypes = [c_void_p, c_void_p, c_int]
-        L.rt_scene_launch_history.restype = c_int
+        if hasattr(L, "rt_scene_launch_history"):  # (older builds loaded through RTC_LIB for an A/B lack it)
+            L.rt_scene_launch_history.argtypes = [c_void_p, c_void_p, c_int]
+            L.rt_scene_launch_history.restype = c_int
         L.rt_scene_kernel.argtypes = [c_void_p]
         L.rt_scene_kernel.restype = c_char_p
         L.rt_scene_check.argtypes = [c_void_p]
@@ -306,6 +307,8 @@ class DeviceScene:
     def launch_history(self, n: int) -> list:
         """Frame-kernel milliseconds of the last min(n, 64) launches, oldest first (rt_scene_launch_history;
         call after they completed)."""
+        if not hasattr(self._L, "rt_scene_launch_history"):
+            return []
         buf = (c_double * max(int(n), 1))()
         m = self._L.rt_scene_launch_history(self._h, buf, int(n))
         if m < 0:

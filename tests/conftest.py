@@ -25,6 +25,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
 
 
+def pytest_collection_modifyitems(config, items):
+    """A per-test time limit (pytest-timeout, when installed) for every test without its own: a test stuck
+    in a GPU call then fails with its name and stack instead of holding the run (thread method: it can
+    interrupt a test blocked inside a HIP call)."""
+    if not config.pluginmanager.hasplugin("timeout") or config.getoption("timeout", None):
+        return
+    for item in items:
+        if item.get_closest_marker("timeout") is None:
+            item.add_marker(pytest.mark.timeout(600, method="thread"))
+
+
 def _make(path, *targets):
     subprocess.run(["make", "-s", "-C", path, "-j8", *targets], check=True)
 
