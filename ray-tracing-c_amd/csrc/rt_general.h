@@ -86,7 +86,9 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
 // every record store used to leave L2 for HBM at >= 32 B.  Only static register indices (unrolled
 // shifts): a dynamically indexed private array would live in scratch.
 #ifndef RT_GEN_EXTRA_SL
-#define RT_GEN_EXTRA_SL 0  // pre_common's extra box actions branch-free (A/B variant)
+// pre_common's extra box actions branch-free (config 5, same box, three rounds: 3243-3262 ms per frame
+// against 3275-3396 with the branches)
+#define RT_GEN_EXTRA_SL 1
 #endif
 #ifndef RT_GEN_WREG
 #define RT_GEN_WREG 4  // pdf weights in registers (config 5, same box: 8 / 4 / 0 -> 274 / 276 / 271 Msamples/s)

@@ -262,8 +262,12 @@ constexpr size_t kLptHistBytes = 8192;
 // §5): the slowest lane chain's latency and the lanes' aggregate throughput per pre-pass traversal
 // step, and a whole-wave chain's rate.
 constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
-// tail shaping at 3 waves per SIMD (the N >= 2 shares): ChainModel.alpha (0: off)
-constexpr float kTailAlpha3 = 0.0f;
+// Tail shaping (ChainModel.alpha) for launches at 3 waves per SIMD with at least kTailPx pixels per lane of
+// the 5-wave grid -- the N = 2 and N = 4 rank shares (1.24 and 0.62; N = 8: 0.31).  Same box, max rank ms,
+// three rounds: N = 2 alpha 0: 164.4-167.1, 1.5: 150.7-153.4, 2: 162.3-165.1, 3: 167.1-169.6;
+// N = 4 0: 94.0-95.3, 1.5: 93.5-94.5; N = 8 (two rounds) 0: 61.0-61.3, 1.5: 62.4-63.1; N = 1 (5 waves) 1.5:
+// 257.6-258.4 vs 252.0-252.8 ms per frame.
+constexpr float kTailAlpha3 = 1.5f, kTailPx = 0.5f;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
@@ -1381,7 +1385,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.thr = kLaneThr;
   m.coop = kCoopStep;
   m.beta = cfg.chain_beta > 0.0f ? cfg.chain_beta : (d->chain_occ == 5 ? 0.9f : 0.7f);
-  m.alpha = cfg.chain_alpha >= 0.0f ? cfg.chain_alpha : (d->chain_occ == 5 ? 0.0f : kTailAlpha3);
+  m.alpha = cfg.chain_alpha >= 0.0f ? cfg.chain_alpha
+            : d->chain_occ == 3 && (double)npix >= kTailPx * (double)d->chain_grid5 * b1::kBlock ? kTailAlpha3 : 0.0f;
   m.floor = cfg.chain_floor;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
