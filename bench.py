@@ -321,7 +321,8 @@ def main():
                          "traffic": (round(pmc["fetch_bytes"] + pmc["write_bytes"])
                                      if pmc and "fetch_bytes" in pmc and "write_bytes" in pmc else None),
                          "pmc": ({k: round(pmc[k], 4) for k in ("valu_busy", "lanes_active", "valu_insts_per_sample",
-                                                                "lds_bank_conflict_frac", "kernel_ms_per_frame")
+                                                                "lds_bank_conflict_frac", "kernel_ms_per_frame",
+                                                                "kernel_ms_per_timed_frame")
                                   if k in pmc} if pmc else pmc_status if pmc_status == "stale" else None),
                          "pmc_source": pmc_src if pmc else None,
                          "build_id": build_id,

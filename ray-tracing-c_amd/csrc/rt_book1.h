@@ -149,6 +149,10 @@ struct Book1View {
   uint32_t *cost_out;        // cost pre-pass: traversal steps per work item, or null
   uint32_t cost_budget;      // cost pre-pass: steps after which a pixel's estimate is extrapolated
   uint32_t *draw_out;        // cost pre-pass (kMode 1): pcg32 draws per work item
+  // the cost pre-pass's samples are the pixel's first samples: it leaves each pixel's colour sum and
+  // position there (pre_word: stream offset | samples << 24), and the chain launch's segment 0 / unsplit
+  // items go on from it instead of rendering them again (null: off)
+  float4 *pre_state;
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
   const uint32_t *coop_waves_dev;  // by the first *coop_waves_dev waves of the grid
@@ -184,6 +188,21 @@ struct Book1View {
 };
 // a record's end word (ch_col[i].w), read as st_rel128 published it
 RT_D uint32_t rec_end(const Book1View &V, uint32_t i) { return ld_rel((const uint32_t *)&V.ch_col[i] + 3); }
+
+using rt::pre_word;
+// A chain launch's item that starts the pixel's true chain at offset 0 -- segment 0 of a split pixel, or
+// an unsplit pixel -- goes on from the pre-pass's position instead: same samples, same summation order
+// (acc = ((0 + c_0) + c_1) + ...), so the pixel is bit-identical and its first samples are not rendered
+// twice.
+RT_D void pre_resume(const Book1View &V, int64_t pix, uint32_t seg, Pcg32 &g, uint32_t &s, f3 &acc) {
+  if (!V.pre_state || !((seg & kItemUnsplit) || seg == 0u)) return;
+  const float4 p = V.pre_state[pix];
+  const uint32_t w = __builtin_bit_cast(uint32_t, p.w), n = w >> 24;
+  if (n == 0u) return;
+  g.skip(w & 0xffffffu);
+  s = n;
+  acc = mk(p.x, p.y, p.z);
+}
 
 // ---------------------------------------------------------------- chain segments
 RT_D uint32_t seg_start(const ChainPx &P, uint32_t t) { return t * P.seg_len; }
@@ -750,8 +769,9 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     g.n = res->n;
     s = res->s, tc = res->tc, st = res->st;
     acc = mk(res->acc[0], res->acc[1], res->acc[2]);
-  } else if (kMode == 2 && !(seg & kItemUnsplit)) {
-    chain_start(V, (uint32_t)pix, seg, g, tc, st);
+  } else if (kMode == 2) {
+    if (!(seg & kItemUnsplit)) chain_start(V, (uint32_t)pix, seg, g, tc, st);
+    pre_resume(V, pix, seg, g, s, acc);
   }
   const bool use_bf = V.n_bf_leaves > 0;
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
@@ -1205,6 +1225,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
           if (kMode == 1) {
             V.cost_out[pix] = cut ? (uint32_t)((uint64_t)px_steps * spp / s) : px_steps;
             V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
+            if (V.pre_state) V.pre_state[pix] = make_float4(acc.x, acc.y, acc.z, u2f(pre_word(g.n, (uint32_t)s)));
           }
           if (V.px_time) V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
@@ -1249,8 +1270,11 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         if (kMode == 2 && cont) {
           g.skip(st);
-        } else if (kMode == 2 && !(seg & kItemUnsplit)) {
-          chain_start(V, (uint32_t)pix, seg, g, tc, st);
+        } else if (kMode == 2) {
+          if (!(seg & kItemUnsplit)) chain_start(V, (uint32_t)pix, seg, g, tc, st);
+          uint32_t s_pre = (uint32_t)s;
+          pre_resume(V, pix, seg, g, s_pre, acc);
+          s = (int)s_pre;
         }
         need_pixel = false;
         px_steps = 0;

@@ -93,6 +93,11 @@ struct Pcg32 {
   RT_D float between(float lo, float hi) { return lo + f32() * (hi - lo); }
 };
 
+// A cost pre-pass's position of a pixel (rt_book1.h pre_resume, rt_general.h): its first s samples, from
+// stream offset 0, in order, by the same code, end at stream offset o.  0: nothing to resume (an offset
+// past 24 bits, or more than 255 samples).
+RT_D uint32_t pre_word(uint32_t o, uint32_t s) { return o < (1u << 24) && s < 256u ? o | (s << 24) : 0u; }
+
 // vec3_rand_between in gcc order: z first, then y, then x (src/vec3.c:33-35)
 RT_D f3 rand_between(Pcg32 &g, float lo, float hi) {
   const float z = g.between(lo, hi);

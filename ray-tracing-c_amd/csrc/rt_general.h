@@ -20,6 +20,8 @@ struct GeneralView {
   int32_t *work_counter;     // zeroed before each launch
   const int32_t *order;      // work item order (longest-first), or null
   uint32_t *cost_out;        // cost pass: rays traced per work item, or null
+  float4 *pre_out;           // cost pass: each pixel's colour sum and position (pre_word), or null
+  const float4 *pre_in;      // the launch after it: pixels go on from there instead of sample 0, or null
   int32_t batch;             // kBatch: shade once this many lanes of a wave wait (RT_GEN_BATCH)
   int32_t steps;             // kBatch: preorder entries per lane per traversal iteration (RT_GEN_STEPS)
   int32_t n_lds;             // kBatch: the first n_lds preorder entries are staged in LDS (RT_GEN_LDS)
@@ -666,7 +668,12 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   bool need_pixel = true, need_sample = true, done = false;
   PreTrace T;  // kBatch: the lane's trace in progress (tracing) or finished, not yet shaded (pending)
   T.found = false;
-  bool tracing = false, pending = false;
+  // the lane's trace state as one integer in a VGPR: as two loop-carried bools the compiler kept lane
+  // masks and merged them (s_andn2 / s_and / s_or) at every trace step
+  enum : int { kIdle = 0, kTracing = 1, kPending = 2 };
+  int tstate = kIdle;
+#define tracing (tstate == kTracing)
+#define pending (tstate == kPending)
   uint64_t gs_c = 0;
   (void)gs_c;
 #ifdef RT_GEN_STATS
@@ -712,6 +719,16 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           pixel_pos = add(add(ld3(S.cam.pixel00), scale(du, (float)i)), scale(dv, (float)j));
           acc = mk(0.0f, 0.0f, 0.0f);
           s = 0;
+          if (V.pre_in) {  // the cost pass rendered this pixel's first samples: on from there (same
+                           // samples, same summation order; rt_book1.h pre_resume)
+            const float4 ps = V.pre_in[pix];
+            const uint32_t w = __builtin_bit_cast(uint32_t, ps.w);
+            if ((w >> 24) != 0u && (int)(w >> 24) < spp) {
+              g.skip(w & 0xffffffu);
+              s = (int)(w >> 24);
+              acc = mk(ps.x, ps.y, ps.z);
+            }
+          }
           rays = 0;
           need_pixel = false;
           need_sample = spp > 0;
@@ -782,10 +799,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
             GS_ADD(kGsCycRare, GS_NOW() - gs_c);
             GS_ADD(kGsRareSteps, run_rare);
-            if (fin) {
-              tracing = false;
-              pending = true;
-            }
+            if (fin) tstate = kPending;
           }
           const uint64_t tr2 = __ballot(!done && tracing), ready2 = __ballot(!done && !tracing);
           const int batch2 = min(V.batch, (3 * (int)__popcll(tr2 | ready2) + 3) / 4);
@@ -846,11 +860,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           gs_c = GS_NOW();
           pre_begin(T, o, d);
           GS_ADD(kGsCycBegin, GS_NOW() - gs_c);
-          tracing = true;
+          tstate = kTracing;
           rays++;
           continue;
         }
-        pending = false;
+        tstate = kIdle;
         found = T.found;
         h = T.h;
       } else {
@@ -917,7 +931,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           depth--;
           if (kBatch && depth > 0) {  // the next bounce's trace starts at once
             pre_begin(T, o, d);
-            tracing = true;
+            tstate = kTracing;
             rays++;
           }
         }
@@ -962,6 +976,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       dst[q] = (uint8_t)(int)(256.0f * v);
     }
     if (V.cost_out) V.cost_out[pix] = rays;
+    if (V.pre_out) V.pre_out[pix] = make_float4(acc.x, acc.y, acc.z, __builtin_bit_cast(float, pre_word(g.n, (uint32_t)s)));
     need_pixel = true;
     GS_ADD(kGsCycWrite, GS_NOW() - gs_c);
   }
@@ -973,6 +988,8 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
 #undef GS_NOW
 #undef GS_ADD
 #undef GS_CNT
+#undef tracing
+#undef pending
 }
 
 }  // namespace gen

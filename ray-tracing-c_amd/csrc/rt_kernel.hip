@@ -602,6 +602,7 @@ enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
   bool lpt = true, bf = true, px_time = false, debug = false;
+  bool pre_resume = true;     // chain items go on from the cost pre-pass's samples (RT_PRE_RESUME=0: off)
   int lpt_spp = 16, shade_batch = 48;
   int mode = kModeAuto;
   // chain_beta: a lane chain's latency target as a fraction of the launch's throughput time; 0 = by
@@ -670,6 +671,7 @@ struct Config {
     c.general = env_flag("RT_GENERAL", true);
     c.gen_pre = env_flag("RT_GEN_PRE", true);
     c.lpt = env_flag("RT_LPT", true);
+    c.pre_resume = env_flag("RT_PRE_RESUME", true);
     c.bf = env_flag("RT_BF", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
@@ -742,6 +744,7 @@ struct rt_device_scene {
   int32_t *lpt_order = nullptr;  // work item order (W*H)
   uint32_t *lpt_hist = nullptr;  // buckets, offsets, whole-wave counters, sums
   uint32_t *draw_out = nullptr;  // pre-pass draws per work item (W*H)
+  float4 *pre_state = nullptr;   // pre-pass colour sum and position per work item (W*H; rt_book1.h pre_resume)
   uint32_t *cost_own = nullptr;  // RT_COST_SMOOTH: the pre-pass's own costs (W*H), lpt_cost the smoothed ones
   DeepRec *deep_rec = nullptr;   // max_depth > kMaxDepth: path records (rt_render_deep_kernel)
   int64_t deep_threads = 0;
@@ -767,6 +770,7 @@ struct rt_device_scene {
   int gen_grid = 0, gen_block = 256;
   float4 *gen_xrec = nullptr;  // explicit path records of the general kernel (rt_general.h: GeneralView.xrec / xw)
   float *gen_xw = nullptr;
+  float4 *gen_pre = nullptr;   // the general cost pass's colour sums and positions per pixel (GeneralView.pre_out)
   void *pre_arena = nullptr;  // the general path's preorder entries (rt_device.h: trace_pre)
   int gen_lds = 0;
   size_t gen_lds_bytes = 0;   // dynamic LDS of the general kernel
@@ -1061,6 +1065,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->lpt_hist = (uint32_t *)(b + off[6]);
   d->draw_out = (uint32_t *)(b + off[7]);
   if (cfg.cost_smooth > 0) HIP_OK(hipMalloc(&d->cost_own, npix * sizeof(uint32_t)));
+  if (cfg.pre_resume) HIP_OK(hipMalloc(&d->pre_state, npix * sizeof(float4)));
+  V.pre_state = nullptr;  // (set per launch: the cost pass writes it, the chain launch after it reads it)
   if (cfg.px_time) {
     HIP_OK(hipMalloc(&d->px_time, npix * 3 * sizeof(uint32_t)));
     V.px_time = d->px_time;
@@ -1158,6 +1164,8 @@ static int general_upload(rt_device_scene *d, const rt_flat_scene *s) {
   const size_t threads = (size_t)d->gen_grid * d->gen_block;
   HIP_OK(hipMalloc(&d->gen_xrec, threads * kMaxDepth * (sizeof(float4) + sizeof(float))));
   d->gen_xw = (float *)(d->gen_xrec + threads * kMaxDepth);
+  if (cfg.pre_resume && cfg.lpt)
+    HIP_OK(hipMalloc(&d->gen_pre, (size_t)s->camera.width * s->camera.height * sizeof(float4)));
   d->general = true;
   if (cfg.debug)
     fprintf(stderr, "[rtc] general persistent kernel: grid=%d (%d/CU) block=%d lds entries=%d of %d, perlin in lds %d, "
@@ -1271,8 +1279,10 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->b1_arena) (void)hipFree(d->b1_arena);
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->gen_xrec) (void)hipFree(d->gen_xrec);
+  if (d->gen_pre) (void)hipFree(d->gen_pre);
   if (d->px_time) (void)hipFree(d->px_time);
   if (d->cost_own) (void)hipFree(d->cost_own);
+  if (d->pre_state) (void)hipFree(d->pre_state);
   if (d->seg_time) (void)hipFree(d->seg_time);
   if (d->mig_q) (void)hipFree(d->mig_q);
   if (d->deep_rec) (void)hipFree(d->deep_rec);
@@ -1292,6 +1302,7 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.S.cam.spp = d->cfg.lpt_spp;
   P.cost_out = d->cost_own ? d->cost_own : d->lpt_cost;
   P.draw_out = d->draw_out;
+  P.pre_state = d->pre_state;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.n_coop = nullptr;
   // at the chain kernel's occupancy, on its grid
@@ -1430,6 +1441,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.ch_px = d->ch_px;
   V.ch_items = d->ch_items;
   V.ch_n_items = d->ch_cnt + kCnItems;
+  V.pre_state = d->pre_state;  // the chain items go on from the pre-pass's samples
   V.ch_seg = d->ch_seg;
   V.ch_col = col;
   V.ch_acc0 = d->ch_acc0;
@@ -1478,6 +1490,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   // continuation items (normally none: the launch exits at once)
   b1::Book1View C = V;
   C.n_coop = nullptr;
+  C.pre_state = nullptr;  // (continuations start from the fold's exact positions)
   C.ch_cont = d->ch_cont;
   C.ch_n_cont = d->ch_cnt + kCnCont;
   C.mig_epoch = ++d->mig_epoch;
@@ -1631,6 +1644,8 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
     G.work_counter = d->gen_counter;
     G.order = nullptr;
     G.cost_out = nullptr;
+    G.pre_out = nullptr;
+    G.pre_in = nullptr;
     G.stats = nullptr;
     G.xrec = d->gen_xrec;
     G.xw = d->gen_xw;
@@ -1641,6 +1656,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
       gen::GeneralView P = G;
       P.S.cam.spp = cfg.lpt_spp;
       P.cost_out = d->lpt_cost;
+      P.pre_out = d->gen_pre;  // (its samples are the pixels' first ones: the launch below goes on from them)
       HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
       launch_general(d, all, gg, gb, st, P, d_out);
       HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
@@ -1652,6 +1668,7 @@ static int render_rows(rt_device_scene *d, int row0, int row_stride, int n_rows,
                          cfg.tile_order ? G.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16);
       HIP_OK(hipGetLastError());
       G.order = d->lpt_order;
+      G.pre_in = d->gen_pre;
     }
     HIP_OK(hipMemsetAsync(d->gen_counter, 0, sizeof(int32_t), st));
 #ifdef RT_GEN_STATS

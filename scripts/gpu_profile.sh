@@ -35,7 +35,7 @@ echo "config $KEY samples/frame $SAMPLES build $BID box $BOX"
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 900 python3 bench.py $CFG
 step stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o run -- \
     python3 bench.py $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-parity
-A="$CFG --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
+A="$CFG --steps 1 --warmup 1 --no-cpu-baseline --no-parity"  # (2 frames: the first pays one-time costs)
 step pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     --output-format csv -d gpurun_out/${TAG}_pmc_sq1 -o run -- python3 bench.py $A
 step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
@@ -50,6 +50,6 @@ timeout -k 10 -s KILL 600 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCC_
   && ATOM=gpurun_out/${TAG}_pmc_atom
 echo "== pmc_atom ${ATOM:-failed}"
 python3 scripts/pmc_summary.py gpurun_out/${TAG}_pmc_${KEY}.json --build-id "$BID" --config "$KEY" --samples-per-frame "$SAMPLES" --box "$BOX" \
-    --stats gpurun_out/${TAG}_stats --stats-frames 3 --pmc-frames 1 \
+    --stats gpurun_out/${TAG}_stats --stats-frames 3 --stats-warmup 1 --pmc-frames 2 \
     gpurun_out/${TAG}_pmc_sq1 gpurun_out/${TAG}_pmc_sq2 gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write $ATOM
 find gpurun_out/${TAG}_stats -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats_${KEY}.csv \;

@@ -6,7 +6,8 @@
 --stats DIR: a `rocprofv3 --kernel-trace --stats` run of `bench.py` (F frames in all, warmup
 included): per kernel the calls, total ns and ms per frame (= total / F; the chain kernel is two
 dispatches per frame, the launch and its -- normally empty -- continuation, so AverageNs is not the
-per-frame time).
+per-frame time), every dispatch's ms, and with --stats-warmup W the ms per frame of the F - W timed
+frames only (kernel_ms_per_timed_frame: what bench.py's HIP events measure).
 --pmc-frames F DIR...: `rocprofv3 --pmc` passes (scripts/gpu_profile.sh), each over F frames.  Sums the
 counter values per kernel over all dispatches of a pass and derives, per kernel:
   valu_insts_per_sample  SQ_INSTS_VALU / (F x S) (wave-level instructions)
@@ -35,6 +36,7 @@ def main():
     ap.add_argument("--samples-per-frame", type=float, required=True)
     ap.add_argument("--stats")
     ap.add_argument("--stats-frames", type=int, default=1)
+    ap.add_argument("--stats-warmup", type=int, default=0, help="frames of the stats run that were warm-up")
     ap.add_argument("--pmc-frames", type=int, default=1)
     ap.add_argument("--box", default="{}", help="JSON: the box the passes ran on (rtc.box_identity)")
     ap.add_argument("pmc", nargs="*")
@@ -54,6 +56,14 @@ def main():
                 if r["Kernel_Name"] in res:  # every dispatch's duration (ms), in order
                     res[r["Kernel_Name"]].setdefault("dispatch_ms", []).append(
                         round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, 4))
+        # per frame of the timed steps only (the warm-up frame's first dispatch also pays one-time costs;
+        # DESIGN.md §6): the dispatches of the last stats_frames - stats_warmup frames
+        timed = a.stats_frames - a.stats_warmup
+        for e in res.values():
+            d = e.get("dispatch_ms")
+            if d and timed > 0 and len(d) % a.stats_frames == 0:
+                per = len(d) // a.stats_frames
+                e["kernel_ms_per_timed_frame"] = sum(d[per * a.stats_warmup:]) / timed
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for d in a.pmc:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):

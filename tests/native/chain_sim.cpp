@@ -6,9 +6,13 @@
 // (random start delays, one sample per scheduling step).  Then the fold and the continuations, as chain_fold_kernel and the continuation launch do.  tests/test_kernel_logic.py compares the image
 // with the oracle: the protocol must be exact whatever the plan and the timing.
 // It is not part of the product and is never linked into librtc_amd.so.
-//   chain_sim <scene> <width> <spp> <depth> <out.rgb> <seed> <kmin> <kmax> <margin> <slack> [pad]
+//   chain_sim <scene> <width> <spp> <depth> <out.rgb> <seed> <kmin> <kmax> <margin> <slack> [pad] [pre]
 // pad > 1: stream-length estimates off by up to 2x are then spread over pad x the estimate (the
 // planner's padded plan for many-segment pixels: segments past the true stream end).
+// pre > 0: a cost pre-pass of `pre` samples per pixel (a random 0..pre of them for some pixels, as the
+// pre-pass's step budget cuts heavy pixels short) leaves its colour sum and position, and segment 0 /
+// unsplit chains go on from there (rt_book1.h: pre_word / pre_resume) -- the pre-pass position can lie
+// past segment 1's start.
 #include "../../ray-tracing-c_amd/csrc/rt_book1.h"
 #include "../../include/rt_hip.h"
 
@@ -74,6 +78,7 @@ int main(int argc, char **argv) {
   const float margin = (float)atof(argv[9]);
   const uint32_t slack = (uint32_t)atoi(argv[10]);
   const double pad = argc > 11 ? atof(argv[11]) : 1.0;
+  const int pre = argc > 12 ? atoi(argv[12]) : 0;
   const void *arrays[13] = {s->bvh,        s->spheres,  s->quads,     s->lists,  s->list_items,
                             s->translates, s->rotates,  s->media,     s->materials, s->textures,
                             s->images,     s->perlins,  s->image_bytes};
@@ -87,6 +92,19 @@ int main(int argc, char **argv) {
   std::vector<float4> col;
   std::vector<float4> acc0(npix);
   std::vector<uint32_t> split;
+  // the pre-pass (kMode 1): the pixel's first samples from offset 0, as the cost kernel leaves them
+  std::vector<float4> pre_state(npix, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  b1::Book1View PV;
+  memset(&PV, 0, sizeof PV);
+  PV.pre_state = pre > 0 ? pre_state.data() : nullptr;
+  for (int p = 0; pre > 0 && p < npix; p++) {
+    Pcg32 g;
+    g.seed((uint64_t)(17 + p / W), (uint64_t)(23 + p % W));
+    const int n = (rnd() % 4u) == 0 ? (int)(rnd() % (uint32_t)(pre + 1)) : pre;
+    f3 a = mk(0.0f, 0.0f, 0.0f);
+    for (int q = 0; q < n; q++) a = add(a, sample(view, p, g));
+    pre_state[p] = make_float4(a.x, a.y, a.z, b1::u2f(b1::pre_word(g.n, (uint32_t)n)));
+  }
   std::vector<Chain> chains;
   uint32_t rec = 0;
   for (int p = 0; p < npix; p++) {
@@ -125,6 +143,7 @@ int main(int argc, char **argv) {
         c.g.skip((uint32_t)k * seg_len);
         if (k + 1 < K) c.tc = (uint32_t)(k + 1) << 24, c.st = (uint32_t)(k + 1) * seg_len;
       }
+      b1::pre_resume(PV, p, c.seg, c.g, c.s, c.acc);
       c.start_at = (int)(rnd() % 64u);
       c.done = false;
       chains.push_back(c);

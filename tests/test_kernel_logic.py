@@ -42,17 +42,21 @@ def test_kernel_code_on_host_matches_oracle(tmp_path, scene, width, spp, depth, 
 CHAIN = os.path.join(ROOT, "tests", "native", "bin", "chain_sim")
 
 
-@pytest.mark.parametrize("scene,width,spp,seed,kmin,kmax,margin,slack,pad", [
-    (1, 48, 64, 1, 2, 8, 1.5, 64, 1.0),    # plain plans
-    (1, 48, 64, 2, 2, 16, 1.0, 1, 1.0),    # lists one record past the plan: most pixels need a continuation
-    (0, 40, 40, 3, 1, 8, 1.2, 4, 1.0),     # the three-spheres scene, unsplit pixels mixed in
-    (1, 48, 32, 4, 4, 32, 1.0, 2, 1.0),    # many short segments
-    (1, 24, 200, 5, 2, 6, 1.5, 64, 1.0),   # long segments
-    (1, 48, 64, 6, 8, 24, 1.5, 64, 1.3),   # padded plans: segments past the stream's true end
-    (1, 24, 200, 7, 8, 16, 1e9, 64, 1.6),  # padded long segments, lists of spp + slack (the planner's)
-    (1, 48, 64, 8, 2, 16, 1.0, 1, 1.3),    # padded plans with tiny lists (continuations)
-    (0, 40, 40, 9, 1, 8, 1.2, 4, 2.0)])    # padded, unsplit pixels mixed in
-def test_chain_protocol_on_host_matches_oracle(tmp_path, scene, width, spp, seed, kmin, kmax, margin, slack, pad):
+@pytest.mark.parametrize("scene,width,spp,seed,kmin,kmax,margin,slack,pad,pre", [
+    (1, 48, 64, 1, 2, 8, 1.5, 64, 1.0, 0),    # plain plans
+    (1, 48, 64, 2, 2, 16, 1.0, 1, 1.0, 0),    # lists one record past the plan: most pixels need a continuation
+    (0, 40, 40, 3, 1, 8, 1.2, 4, 1.0, 0),     # the three-spheres scene, unsplit pixels mixed in
+    (1, 48, 32, 4, 4, 32, 1.0, 2, 1.0, 0),    # many short segments
+    (1, 24, 200, 5, 2, 6, 1.5, 64, 1.0, 0),   # long segments
+    (1, 48, 64, 6, 8, 24, 1.5, 64, 1.3, 0),   # padded plans: segments past the stream's true end
+    (1, 24, 200, 7, 8, 16, 1e9, 64, 1.6, 0),  # padded long segments, lists of spp + slack (the planner's)
+    (1, 48, 64, 8, 2, 16, 1.0, 1, 1.3, 0),    # padded plans with tiny lists (continuations)
+    (0, 40, 40, 9, 1, 8, 1.2, 4, 2.0, 0),     # padded, unsplit pixels mixed in
+    (1, 48, 64, 10, 2, 8, 1.5, 64, 1.0, 16),  # segment 0 / unsplit chains go on from the pre-pass's 16 samples
+    (1, 48, 64, 11, 8, 32, 1.0, 2, 1.0, 16),  #   ... with many short segments: the pre-pass ends past segment 1's start
+    (1, 48, 64, 12, 2, 16, 1.0, 1, 1.3, 8),   #   ... with padded plans and tiny lists (continuations)
+    (0, 40, 40, 13, 1, 8, 1.2, 4, 2.0, 16)])  #   ... unsplit pixels mixed in
+def test_chain_protocol_on_host_matches_oracle(tmp_path, scene, width, spp, seed, kmin, kmax, margin, slack, pad, pre):
     """The chain render's protocol (rt_book1.h: chain_boundary / chain_couple / chain_walk_done /
     chain_record) on the host under ASan, with random segment counts, stream-length estimates off by up
     to 2x (and padded plans, whose last segments start past the true stream end), tiny record lists and
@@ -61,7 +65,7 @@ def test_chain_protocol_on_host_matches_oracle(tmp_path, scene, width, spp, seed
     out = str(tmp_path / "c.rgb")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
     r = subprocess.run([CHAIN, str(scene), str(width), str(spp), "50", out, str(seed), str(kmin), str(kmax), str(margin),
-                        str(slack), str(pad)], capture_output=True, text=True, env=env, timeout=600)
+                        str(slack), str(pad), str(pre)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     sc = rtc.Scene.preset(scene, width, spp, 50)
     ref = pyoracle.render(sc)
