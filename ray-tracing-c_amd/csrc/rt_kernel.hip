@@ -604,6 +604,13 @@ struct Config {
   bool lpt = true, bf = true, px_time = false, debug = false;
   bool pre_resume = true;     // chain items go on from the cost pre-pass's samples (RT_PRE_RESUME=0: off)
   int lpt_spp = 16, shade_batch = 48;
+  // the chain launch's cost pre-pass spp (capped at a quarter of the frame's; lpt_spp is the least a chain
+  // launch needs): its samples are the frame's first ones (pre_resume), so a longer pre-pass only costs its
+  // lower efficiency and buys a better plan -- headline, same box, two-three rounds: 16 spp 3252-3267
+  // Msamples/s, 32 3293-3304, 48 3297-3313, 64 3322-3330, 128 3326-3330 (the 6000-step budget stops most
+  // pixels near 44 samples); the general path's longest-first pre-pass stays at lpt_spp (config 5: 16 spp
+  // 302-311, 32 304-307, 64 293-300).  RT_LPT_SPP sets both.
+  int chain_pre_spp = 64;
   int mode = kModeAuto;
   // chain_beta: a lane chain's latency target as a fraction of the launch's throughput time; 0 = by
   // the launch's occupancy: 0.9 at 5 waves per SIMD (N = 1: fewer splits, same box 244.6-245.2 vs
@@ -642,6 +649,7 @@ struct Config {
     // the documented planner / scheduling parameters
     c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
     if (c.lpt_spp < 1) c.lpt_spp = 1;
+    if (getenv("RT_LPT_SPP")) c.chain_pre_spp = c.lpt_spp;
     c.chain_beta = env_float("RT_CHAIN_BETA", c.chain_beta);
     c.chain_alpha = env_float("RT_CHAIN_ALPHA", c.chain_alpha);
     c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
@@ -1297,9 +1305,18 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
 }
 
 // ------------------------------------------------------------------------------ launches
+// The chain launch's cost pre-pass spp (Config.chain_pre_spp, at most a quarter of the frame's spp, at
+// least lpt_spp; the exact-plan diagnostic: the frame's spp).
+static int chain_pre_spp(const rt_device_scene *d, int spp) {
+  const Config &c = d->cfg;
+  if (c.lpt_spp >= spp) return spp;
+  const int p = c.chain_pre_spp < spp / 4 ? c.chain_pre_spp : spp / 4;
+  return p > c.lpt_spp ? p : c.lpt_spp;
+}
+
 static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t *d_out, hipStream_t st) {
   (void)hipMemsetAsync(P.work_counter, 0, kCounterBytes, st);  // (the previous launch left it past its items)
-  P.S.cam.spp = d->cfg.lpt_spp;
+  P.S.cam.spp = chain_pre_spp(d, P.S.cam.spp);
   P.cost_out = d->cost_own ? d->cost_own : d->lpt_cost;
   P.draw_out = d->draw_out;
   P.pre_state = d->pre_state;
@@ -1390,7 +1407,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
                        V.S.cam.width, cfg.cost_smooth);
   hipLaunchKernelGGL(lpt_hist_kernel, dim3(nb), dim3(256), 0, st, d->lpt_cost, n, d->lpt_hist, sums);
   ChainModel m;
-  m.ratio = (float)V.S.cam.spp / (float)cfg.lpt_spp;
+  m.ratio = (float)V.S.cam.spp / (float)chain_pre_spp(d, V.S.cam.spp);
   m.grid_waves = d->chain_grid * (b1::kBlock / 64);
   m.lat = kLaneLat;
   m.thr = kLaneThr;

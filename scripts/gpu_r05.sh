@@ -4,8 +4,9 @@
 #   BENCH=1      the default bench line (N=1, parity-checked)
 #   AB="ab/r03.so;tree;diag:RT_LEAF_MIN=16"  same-box A/B of library builds / diag settings, ROUNDS rounds
 #   AB7="..."    the same on config 5 (scene 7)
-#                (entries: a path, "tree" = the product library, "diag:<VAR=V ...>" = the diagnostic build
-#                under those variables); BENCH_ARGS for other configurations
+#                (entries: a path, "tree" = the product library, "env:<VAR=V ...>" = it under those
+#                variables, "diag:<VAR=V ...>" = the diagnostic build under them); BENCH_ARGS for other
+#                configurations
 #   S7=1         the config-5 bench line (scene 7)
 #   SHARD=1      the per-rank shard probe (WORLDS, default 2,4,8)
 #   PAIRS="8:7 1:0"  chain timelines (diagnostic build), rows saved; EXACT=1 also with the exact plan
@@ -29,6 +30,7 @@ ab() {  # ab "<entries>" "<bench args>"
       case "$e" in
         tree) lib="" ;;
         diag:*) lib=ray-tracing-c_amd/librtc_amd_diag.so; vars="${e#diag:}" ;;
+        env:*) lib=""; vars="${e#env:}" ;;  # the product library under documented parameters
         *) lib="$e" ;;
       esac
       if [ -n "$lib" ]; then export RTC_LIB=$GRAFT_REPO_ROOT/$lib; else unset RTC_LIB; fi
