@@ -289,7 +289,10 @@ def main():
         value = frame_samples * args.steps / elapsed / 1e6
         ops = OPS_PER_SAMPLE.get(args.scene)
         launch_samples = n_rows * W * spp
-        achieved = (launch_samples * ops / (kernel_ms / 1e3) / 1e12) if ops else None
+        # over the step's kernels: the cost pre-pass renders each pixel's first samples and the frame kernel
+        # goes on from them, so the samples of a launch are shared by both -- the step's HIP
+        # events (pre-pass, plan, frame kernel, fold) are the time of the whole launch's work
+        achieved = (launch_samples * ops / (step_ms / 1e3) / 1e12) if ops else None
         workload = (f"Book-1 final scene (reference CLI scene 1) {W}x{H}, {spp} spp, depth {args.depth}"
                     if args.scene == 1 else f"reference scene {args.scene} {W}x{H}, {spp} spp, depth {args.depth}")
         config_key = f"s{args.scene}_{W}x{H}_{spp}spp_d{args.depth}_n{world}"
@@ -331,6 +334,9 @@ def main():
                          "kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
                          "algorithmic_work": f"{ops:.0f} FP32 ops/sample (SURVEY §8d) x {launch_samples} samples/launch"
                          if ops else None,
+                         "achieved_basis": "samples per launch x ops / step_ms_avg (HIP events around the step: cost "
+                                           "pre-pass, plan, frame kernel, fold -- the pre-pass renders the pixels' "
+                                           "first samples, the frame kernel the rest)",
                          "note": "VALU-bound branchy FP32 + u64 integer work, no MFMA, scene in LDS (HBM roof does "
                                  "not apply). peak = dense f32 rate (FMA = 2); issue_ceiling = non-FMA non-packed "
                                  "VALU lane-ops/s (256 CU x 4 SIMD x 32 lanes x 2.4 GHz), the realistic ceiling for "

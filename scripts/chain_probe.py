@@ -60,8 +60,6 @@ if sp.any():
     lastseg = sp & (r[:, 1] + 1 == r[:, 2])
     ratio = r[lastseg, 6] / (spp / r[lastseg, 2])
     print(f"  last segments: records / (spp/K) p50/p90/p99/max {np.percentile(ratio, [50, 90, 99, 100]).round(2)}", flush=True)
-    est = r[sp, 10].astype(np.float64) * r[sp, 2]
-    print(f"  planned stream (seg_len*K) / (pre-pass draws * spp/8) p50 {np.median(est / np.maximum(1, r[sp, 11] * spp / 8)):.2f}", flush=True)
 # items in flight over time (lanes: 64 per wave of the grid); whole-wave items count 64
 ts = np.arange(0.0, end.max() + 5.0, 5.0)
 w = np.where(r[:, 3] >= 1, 64, 1)
