@@ -153,6 +153,10 @@ struct Book1View {
   // position there (pre_word: stream offset | samples << 24), and the chain launch's segment 0 / unsplit
   // items go on from it instead of rendering them again (null: off)
   float4 *pre_state;
+  // the cost pre-pass of a chain launch: its waves, once out of pixels, set the record arena's first
+  // *clean_n records (what the previous chain launch reserved) back to kRecFill (null: off)
+  float4 *clean_col;
+  const uint32_t *clean_n;
   const uint32_t *n_coop;    // chain launches: the first *n_coop of ch_items go to whole waves
   int32_t *coop_counter;     //   (coop_items), claimed through this counter
   const uint32_t *coop_waves_dev;  // by the first *coop_waves_dev waves of the grid
@@ -604,6 +608,29 @@ RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, f
     }
   }
   return __ballot(bad) == 0;
+}
+
+// The record arena is clean (every record's end word kRecFill) between chain launches: a chain launch
+// reserves and may write records [0, n) (n: chain_plan_kernel's reservations), and the next launch's
+// cost pre-pass sets them back, in the waves that have run out of pixels -- at N >= 2 most of the
+// pre-pass's waves idle from the start (0.4 pixels per lane at N = 8), so the 4-5 GB of a share's
+// reservation are written while the pre-pass's heaviest pixels run instead of after the plan (the
+// chain_fill_kernel of r01-r05: 0.9 ms per N = 8 share).  Claims of kCleanChunk records per wave.
+constexpr uint32_t kCleanChunk = 16384;
+__attribute__((noinline)) RT_D void clean_records(float4 *col, const uint32_t *n_p, unsigned long long *ctr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t n = *n_p;
+  const int lane = __lane_id();
+  const float4 fill = make_float4(0.0f, 0.0f, 0.0f, u2f(kRecFill));
+  for (;;) {
+    unsigned long long c0 = 0;
+    if (lane == 0) c0 = atomicAdd(ctr, (unsigned long long)kCleanChunk);
+    c0 = __shfl(c0, 0);
+    if (c0 >= n) return;
+    const uint64_t c1 = c0 + kCleanChunk < n ? c0 + kCleanChunk : n;
+    for (uint64_t i = c0 + (uint64_t)lane; i < c1; i += 64) col[i] = fill;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- chain protocol (kMode 2)
@@ -1351,6 +1378,8 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
       for (int q = 0; q < 6; q++) atomicAdd(V.loop_stats + 24 + q, (unsigned long long)st_step[q]);
   }
 #endif
+  if (kMode == 1 && V.clean_col)  // (the counter: the work-counter line's second half, zeroed with it)
+    clean_records(V.clean_col, V.clean_n, (unsigned long long *)(V.work_counter + 16));
   if (kMode == kMigMode && V.mig_live > 0) {
     // (not inlined, so that the whole-wave code does not enlarge the lane loop's register budget; it
     // reads the view from the kernel argument segment -- V is the kernels' first argument -- because
@@ -1359,15 +1388,15 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
   }
 }
 
-// After a chain launch: one wave per split pixel follows the links from segment 0 and sums the
-// records in sample order (lanes load 64 records, the fold is serial in lane order); a pixel whose
-// links end before spp samples becomes a continuation item (exact position, colour sum so far).
-RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out, ChainCont *cont, uint32_t *n_cont) {
-  const int lane = __lane_id();
+// After a chain launch: one lane per split pixel follows the links from segment 0 and sums the
+// records in sample order; returns true when the pixel is complete (written to out), else q is its
+// continuation item (the exact position its links reach, the colour sum so far).  A segment's records
+// are contiguous: eight 16-B loads are in flight before their eight adds, in order.
+RT_D bool chain_fold_px(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out, ChainCont &q) {
   const uint32_t spp = (uint32_t)V.S.cam.spp;
   const ChainPx P = V.ch_px[pix];
   uint64_t w = V.ch_seg[P.end0];
-  if ((w & kEndEnded) && (w & kEndNoLink)) return;  // segment 0 wrote the pixel itself
+  if ((w & kEndEnded) && (w & kEndNoLink)) return true;  // segment 0 wrote the pixel itself
   f3 acc = mk(0.0f, 0.0f, 0.0f);
   uint32_t total = 0, o = 0;
   bool linked = (w & kEndEnded) != 0;  // (segment 0 always ends; not ended would be a bug: start over)
@@ -1384,13 +1413,18 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     w = V.ch_seg[P.end0 + t];
     const uint32_t n = end_n(w);
     const uint32_t m = n > c ? min(n - c, spp - total) : 0u;
-    for (uint32_t b = 0; b < m; b += 64) {
-      float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (b + (uint32_t)lane < m) r = V.ch_col[rec_index(P, t, c + b + (uint32_t)lane)];
-      const uint32_t cnt = min(64u, m - b);
-      for (uint32_t q = 0; q < cnt; q++)
-        acc = add(acc, mk(lane_bcast(r.x, (int)q), lane_bcast(r.y, (int)q), lane_bcast(r.z, (int)q)));
-      o = __float_as_uint(lane_bcast(r.w, (int)cnt - 1));
+    const float4 *rp = V.ch_col + rec_index(P, t, c);
+    uint32_t i = 0;
+    for (; i + 8u <= m; i += 8u) {
+      float4 r[8];
+      for (int j = 0; j < 8; j++) r[j] = rp[i + j];
+      for (int j = 0; j < 8; j++) acc = add(acc, mk(r[j].x, r[j].y, r[j].z));
+      o = f2u(r[7].w);
+    }
+    for (; i < m; i++) {
+      const float4 r = rp[i];
+      acc = add(acc, mk(r.x, r.y, r.z));
+      o = f2u(r.w);
     }
     total += m;
     if (total >= spp) break;
@@ -1401,15 +1435,12 @@ RT_D void chain_fold(const Book1View &V, uint32_t pix, uint8_t *__restrict__ out
     t = end_t(w), c = end_c(w);
   }
   if (total >= spp) {
-    if (lane == 0) write_pixel(out + (size_t)pix * 3, acc, (int)spp);
-    return;
+    write_pixel(out + (size_t)pix * 3, acc, (int)spp);
+    return true;
   }
-  if (lane == 0) {
-    ChainCont q;
-    q.pix = pix, q.o = o, q.s = total, q.pad = 0u;
-    q.acc[0] = acc.x, q.acc[1] = acc.y, q.acc[2] = acc.z, q.acc[3] = 0.0f;
-    cont[atomicAdd(n_cont, 1u)] = q;
-  }
+  q.pix = pix, q.o = o, q.s = total, q.pad = 0u;
+  q.acc[0] = acc.x, q.acc[1] = acc.y, q.acc[2] = acc.z, q.acc[3] = 0.0f;
+  return false;
 }
 
 }  // namespace b1

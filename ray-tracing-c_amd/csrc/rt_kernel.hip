@@ -99,19 +99,22 @@ __global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_chain_kernel(b1::Bo
   b1::render_batched<kLds, 2>(V, out, lds);
 }
 // The cost pre-pass: the same loop at low spp, under its own name so profiles separate it.
-template <bool kLds>
-__global__ __launch_bounds__(b1::kBlock, 5) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
+template <bool kLds, int kOcc = 5>
+__global__ __launch_bounds__(b1::kBlock, kOcc) void rt_book1_cost_kernel(b1::Book1View V, uint8_t *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   b1::render_batched<kLds, 1>(V, out, lds);
 }
-// After a chain launch: one wave per split pixel (rt_book1.h: chain_fold).
-__global__ __launch_bounds__(256) void chain_fold_kernel(b1::Book1View V, uint8_t *__restrict__ out,
-                                                         const uint32_t *split, const uint32_t *cnt,
-                                                         b1::ChainCont *cont, uint32_t *n_cont) {
+// After a chain launch: one lane per split pixel (rt_book1.h: chain_fold_px).  (One wave per pixel, its
+// lanes loading 64 records for a serial fold in lane order, took 1.44 ms for the N = 8 share's 101 k
+// pixels: 17 dependent load round trips per pixel, 12 pixels per wave in turn.)
+__global__ __launch_bounds__(64) void chain_fold_kernel(b1::Book1View V, uint8_t *__restrict__ out,
+                                                        const uint32_t *split, const uint32_t *cnt,
+                                                        b1::ChainCont *cont, uint32_t *n_cont) {
   const uint32_t n = cnt[1];
-  const uint32_t waves = gridDim.x * (blockDim.x / 64);
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < n; w += waves)
-    b1::chain_fold(V, split[w], out, cont, n_cont);
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    b1::ChainCont q;
+    if (!b1::chain_fold_px(V, split[k], out, q)) cont[atomicAdd(n_cont, 1u)] = q;
+  }
 }
 
 // Persistent general kernel (rt_general.h): grid = resident workgroups, lanes steal pixels.
@@ -268,6 +271,12 @@ constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
 // N = 4 0: 94.0-95.3, 1.5: 93.5-94.5; N = 8 (two rounds) 0: 61.0-61.3, 1.5: 62.4-63.1; N = 1 (5 waves) 1.5:
 // 257.6-258.4 vs 252.0-252.8 ms per frame.
 constexpr float kTailAlpha3 = 1.5f, kTailPx = 0.5f;
+// Heavy pixels (ChainModel.heavy) at 3 waves per SIMD: a pixel planned at >= 8 lane segments gets twice as
+// many.  Its waves hold only heavy lanes (image-tile order) and run up to 3x slower per traversal step than
+// the planner's model (N = 8 rank 7: 0.45-0.70 ms per sample for 340-670 steps).  Same box,
+// N = 8 max rank ms, two rounds: off 60.9 / 60.5, 1.5: 60.7 / 59.7, 2: 59.7 / 59.4, 2 from 4 segments: 64.6 /
+// 64.1; N = 2 unchanged (147-148).
+constexpr float kHeavy3 = 2.0f;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
@@ -339,7 +348,7 @@ __device__ void bitonic_desc(K *key, T *val, int m) {
 //   chain_scan_kernel     offsets (whole-wave items first, then lane items longest first) and the
 //                         whole-wave kernel's wave count;
 //   chain_scatter_kernel  the items, a pixel's K chains adjacent (they start together);
-//   chain_wave_sort_kernel, chain_fill_kernel.
+//   chain_wave_sort_kernel, chain_dirty_kernel.
 // Counters (u32, ch_cnt): see kCn* below; [256, 512) lane bucket counts, [512, 768) their offsets.
 enum : int {
   kCnItems = 0, kCnSplit = 1, kCnFilled = 2, kCnRec = 14 /* u64 */, kCnSeg = 3, kCnCont = 4, kCnWave = 5, kCnWaveNext = 6,
@@ -364,6 +373,10 @@ struct ChainModel {
                         // F_b = the share of the launch's work in costlier buckets (they start before it)
   float pad;            // pixels of >= pad_k segments: segments of the planned length over pad x the estimate
   int pad_k;
+  float cover;          // pixels of >= cover_k segments: segments up to max(own, estimate) x cover (0: off)
+  int cover_k;
+  float heavy;          // lane pixels of >= heavy_k segments: heavy x as many (shorter) segments (1: off)
+  int heavy_k;
   int bucket_shift;     // cost buckets merged 2^this at a time (coarser buckets: longer runs of one image tile)
   uint32_t rec_cap;     // records available
   uint32_t seg_cap;     // end words available
@@ -410,6 +423,9 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
       K = min((int)fminf(ceilf((float)c / cstar_w), 1e6f), m.kmax_wave);
     }
     if (!wave && K < m.kmin) K = m.kmin;  // fill: at least kmin segments when pixels are fewer than lanes
+    // heavy pixels run slower per traversal step than the model says (their waves hold only heavy
+    // lanes: DESIGN.md §5.2), so their lane segments are made shorter still
+    if (!wave && m.heavy > 1.0f && K >= m.heavy_k) K = min(m.kmax_lane, (int)ceilf((float)K * m.heavy));
     K = min(K, max(m.kmax_lane, m.kmax_wave));  // (the item and end-word arrays are sized for this)
     K = max(1, min(K, m.spp / m.min_seg));
     // the stream's length at full spp: the pre-pass draws per sample, averaged over the pixel's row
@@ -437,6 +453,16 @@ __global__ __launch_bounds__(256) void chain_plan_kernel(const uint32_t *cost, c
     }
     seg_len = (seg_len + 1u) & ~1u;  // even: most draw counts are even
     if (seg_len < 2u) K = 1;
+    // covered plan: a pixel whose own pre-pass stream is longer than its neighbours' average (the
+    // estimate) gets more segments of the same length, up to max(own, estimate) x cover, so that its
+    // true end falls inside one of them instead of the last segment running the difference alone
+    if (m.cover > 0.0f && K >= m.cover_k && K > 1) {
+      const double own = (double)draws[p] * m.ratio * m.est_scale;
+      const double reach = fmax(own, est) * m.cover;
+      const int kcap = max(K, min(wave ? m.kmax_wave : max(m.kmax_lane, m.kmax_wave), m.spp / m.min_seg));
+      const int kc = (int)fmin(ceil(reach / seg_len), (double)kcap);
+      if (kc > K && (double)kc * seg_len * 2.0 < 4294967295.0) K = kc;
+    }
     if (K > 1) {
       // a segment holds at most the pixel's spp true samples (+ its garbage samples before it couples):
       // with spp + slack records no list fills up whatever the estimate's error (margin < 1 in tests
@@ -552,13 +578,14 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
   for (int i = threadIdx.x; i < n; i += blockDim.x) items[i] = make_uint2((uint32_t)(val[i] >> 32), (uint32_t)val[i]);
 }
 
-// every planned record's end word = kRecFill; cnt[kCnFilled] = the end of the filled range.
-__global__ void chain_fill_kernel(uint32_t *cnt, float4 *ch_col, uint32_t cap) {
+// The records this launch reserved (and may write), for the next launch's cost pre-pass to set back to
+// kRecFill (rt_book1.h: clean_records; the arena is clean when the launch starts).
+__global__ void chain_dirty_kernel(uint32_t *cnt, uint32_t *dirty, uint32_t cap) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
-  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kCnFilled] = n;
-  const float4 fill = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(b1::kRecFill));
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ch_col[i] = fill;
+  cnt[kCnFilled] = n;
+  *dirty = n;
 }
 
 constexpr size_t kCounterBytes = 128 + b1::kMigWords * sizeof(uint32_t);  // work counter line + migration words
@@ -622,6 +649,13 @@ struct Config {
   float chain_alpha = -1.0f, chain_floor = 0.1f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
+  // chain_cover: pixels of >= chain_cover_k segments get segments up to max(own, estimate) x this (0: off);
+  // chain_heavy: lane pixels of >= chain_heavy_k segments get this x as many (< 1: by occupancy, kHeavy3 at 3
+  // waves per SIMD, off at 5; 1: off)
+  float chain_cover = 1.1f;
+  int chain_cover_k = 8;
+  float chain_heavy = -1.0f;
+  int chain_heavy_k = 8;
   float chain_pad = 1.2f;  // padded plan (chain_plan_kernel; 1: off) for pixels of >= chain_pad_k segments
   int chain_pad_k = 8;
   float chain_fill = 1.0f;   // kmin = ceil(lanes x fill / pixels) segments per pixel (0: off)
@@ -654,6 +688,10 @@ struct Config {
     c.chain_alpha = env_float("RT_CHAIN_ALPHA", c.chain_alpha);
     c.chain_floor = env_float("RT_CHAIN_FLOOR", c.chain_floor);
     c.chain_occ = env_int("RT_CHAIN_OCC", c.chain_occ);
+    c.chain_heavy = env_float("RT_CHAIN_HEAVY", c.chain_heavy);
+    c.chain_cover = env_float("RT_CHAIN_COVER", c.chain_cover);
+    c.chain_cover_k = env_int("RT_CHAIN_COVER_K", c.chain_cover_k);
+    c.chain_heavy_k = env_int("RT_CHAIN_HEAVY_K", c.chain_heavy_k);
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
@@ -763,6 +801,7 @@ struct rt_device_scene {
   // chain render scratch (rt_book1.h: ChainPx), sized for the whole frame at upload; records on demand
   void *ch_arena = nullptr;
   uint32_t *ch_cnt = nullptr, *ch_k = nullptr, *ch_split = nullptr;
+  uint32_t *ch_dirty = nullptr;  // records the last chain launch reserved (the next pre-pass cleans them)
   b1::ChainPx *ch_px = nullptr;
   uint2 *ch_items = nullptr;
   uint64_t *ch_seg = nullptr, *ch_wave_key = nullptr;
@@ -1088,7 +1127,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     const int kmax = cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave;
     const size_t nitem = npix * (size_t)kmax, nseg = npix * (size_t)kmax;
     d->ch_seg_cap = nseg < 0xffffffffu ? (uint32_t)nseg : 0xffffffffu;
-    const size_t cs[9] = {kCnWords * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
+    const size_t cs[9] = {(kCnWords + 64) * sizeof(uint32_t), npix * sizeof(uint32_t), npix * sizeof(uint32_t),
                           npix * sizeof(b1::ChainPx), nitem * sizeof(uint2), nseg * sizeof(uint64_t),
                           nitem * sizeof(uint64_t), npix * sizeof(float4), npix * sizeof(b1::ChainCont)};
     size_t co[9], ct = 0;
@@ -1096,6 +1135,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     HIP_OK(hipMalloc(&d->ch_arena, ct));
     char *c = (char *)d->ch_arena;
     d->ch_cnt = (uint32_t *)(c + co[0]);
+    d->ch_dirty = d->ch_cnt + kCnWords;  // (past the words each plan zeroes)
+    HIP_OK(hipMemset(d->ch_dirty, 0, sizeof(uint32_t)));
     d->ch_k = (uint32_t *)(c + co[1]);
     d->ch_split = (uint32_t *)(c + co[2]);
     d->ch_px = (b1::ChainPx *)(c + co[3]);
@@ -1322,8 +1363,16 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.pre_state = d->pre_state;
   P.cost_budget = d->cfg.cost_budget > 0 ? (uint32_t)d->cfg.cost_budget : 0xffffffffu;
   P.n_coop = nullptr;
+  P.clean_col = (float4 *)d->ch_rec_arena;  // the previous chain launch's records back to kRecFill
+  P.clean_n = d->ch_dirty;
   // at the chain kernel's occupancy, on its grid
+  // (the 3-wave instantiation, like the chain kernel's, spills nothing: N = 8 share pre-pass 4.3 ms at 5)
   const dim3 g((unsigned)d->chain_grid), blk(b1::kBlock);
+  if (d->chain_occ == 3) {
+    if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true, 3>), g, blk, d->b1_lds_bytes, st, P, d_out);
+    else hipLaunchKernelGGL((rt_book1_cost_kernel<false, 3>), g, blk, 0, st, P, d_out);
+    return;
+  }
   if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true>), g, blk, d->b1_lds_bytes, st, P, d_out);
   else hipLaunchKernelGGL((rt_book1_cost_kernel<false>), g, blk, 0, st, P, d_out);
 }
@@ -1342,7 +1391,7 @@ static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V
 
 // Records of a chain launch: grown on demand, up to the RT_CHAIN_MB budget (the planner keeps
 // pixels whole when they run out).
-static int chain_records(rt_device_scene *d, size_t npix, int spp) {
+static int chain_records(rt_device_scene *d, size_t npix, int spp, hipStream_t st) {
   const Config &cfg = d->cfg;
   const size_t kmax = (size_t)(cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave);
   const double seg_recs = fmin((double)cfg.chain_margin * spp / 2.0, (double)spp) + cfg.chain_slack;
@@ -1357,6 +1406,10 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp) {
   d->ch_rec_cap = 0;
   HIP_OK(hipMalloc(&d->ch_rec_arena, want * sizeof(float4) + 256));
   d->ch_rec_cap = want;
+  // a fresh arena: every word kRecFill (0xff bytes; colours are read only from written records), and
+  // nothing for the next pre-pass to set back
+  HIP_OK(hipMemsetAsync(d->ch_rec_arena, 0xff, want * sizeof(float4), st));
+  HIP_OK(hipMemsetAsync(d->ch_dirty, 0, sizeof(uint32_t), st));
   return 0;
 }
 
@@ -1386,7 +1439,7 @@ static hipError_t mark_launch(rt_device_scene *d, int which, hipStream_t st) {
 
 static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hipStream_t st, int64_t npix) {
   const Config &cfg = d->cfg;
-  if (chain_records(d, (size_t)npix, V.S.cam.spp) != 0) return -1;
+  if (chain_records(d, (size_t)npix, V.S.cam.spp, st) != 0) return -1;
   // waves per SIMD: 5 hide more latency (headline frame 266 vs 275 ms at 4), 3 run each lane chain
   // faster with no spills at all (168 VGPRs) -- what a launch with few pixels per lane needs (its time
   // is its longest chains)
@@ -1422,6 +1475,10 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.smooth = cfg.chain_smooth;
   m.est_scale = cfg.chain_est;
   m.pad = cfg.chain_pad;
+  m.cover = cfg.chain_cover;
+  m.cover_k = cfg.chain_cover_k < 2 ? 2 : cfg.chain_cover_k;
+  m.heavy = cfg.chain_heavy >= 1.0f ? cfg.chain_heavy : (d->chain_occ == 3 ? kHeavy3 : 1.0f);
+  m.heavy_k = cfg.chain_heavy_k < 2 ? 2 : cfg.chain_heavy_k;
   m.pad_k = cfg.chain_pad_k < 2 ? 2 : cfg.chain_pad_k;
   m.kmax_lane = cfg.chain_kmax;
   {  // enough items to give every lane of the grid one: light pixels' 1000-sample chains were the
@@ -1445,7 +1502,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
                      d->ch_wave_key, cfg.tile_order ? V.S.cam.width : 0, cfg.tile_order ? cfg.tile_order : 16,
                      m.bucket_shift);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
-  hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, d->ch_cnt, col, (uint32_t)d->ch_rec_cap);
+  hipLaunchKernelGGL(chain_dirty_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, d->ch_dirty, (uint32_t)d->ch_rec_cap);
   HIP_OK(hipGetLastError());
   if (cfg.debug) {  // diagnostic: synchronous peek at the plan
     uint32_t c[16];
@@ -1500,7 +1557,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
               (unsigned long long)pushed, (unsigned long long)popped, mw[b1::kMigDone]);
     }
   }
-  hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 4 + 1 < 2048 ? npix / 4 + 1 : 2048)), dim3(256), 0, st,
+  hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 64 + 1 < 8192 ? npix / 64 + 1 : 8192)), dim3(64), 0, st,
                      V, d_out, (const uint32_t *)d->ch_split, (const uint32_t *)d->ch_cnt, d->ch_cont,
                      d->ch_cnt + kCnCont);
   if (cfg.debug) HIP_OK(hipEventRecord(dbg_ev[1], st));

@@ -196,10 +196,8 @@ int main(int argc, char **argv) {
       fprintf(stderr, "pixel %u: segment 0 never ended\n", p);
       return 3;
     }
-    f3 acc = mk(acc0[p].x, acc0[p].y, acc0[p].z);
-    uint32_t total = b1::end_n(w), t = b1::end_t(w), c = b1::end_c(w);
-    uint32_t o = c == 0 ? b1::seg_start(P, t) : b1::f2u(col[b1::rec_index(P, t, c - 1)].w);
-    for (;;) {
+    // the links must reach forward through ended segments (a protocol bug otherwise)
+    for (uint32_t t = b1::end_t(w), it = 0; !(w & b1::kEndNoLink) && it < P.K; it++) {
       if (t == 0 || t >= P.K) {
         fprintf(stderr, "pixel %u: bad link %u\n", p, t);
         return 3;
@@ -209,23 +207,16 @@ int main(int argc, char **argv) {
         fprintf(stderr, "pixel %u: segment %u never ended\n", p, t);
         return 3;
       }
-      const uint32_t n = b1::end_n(w);
-      for (uint32_t q = c; q < n && total < (uint32_t)spp; q++) {
-        const float4 r = col[b1::rec_index(P, t, q)];
-        acc = add(acc, mk(r.x, r.y, r.z));
-        o = b1::f2u(r.w);
-        total++;
-      }
-      if (total >= (uint32_t)spp || (w & b1::kEndNoLink)) break;
-      t = b1::end_t(w), c = b1::end_c(w);
+      t = b1::end_t(w);
     }
-    if (total < (uint32_t)spp) {  // continuation: the true chain from (o, total, acc)
-      n_cont++;
-      Pcg32 g;
-      g.seed((uint64_t)(17 + p / W), (uint64_t)(23 + p % W));
-      g.skip(o);
-      for (; total < (uint32_t)spp; total++) acc = add(acc, sample(view, (int)p, g));
-    }
+    b1::ChainCont q;  // the kernel's fold (chain_fold_kernel: chain_fold_px) into the image
+    if (b1::chain_fold_px(V, p, img.data(), q)) continue;
+    n_cont++;  // continuation: the true chain from (o, s, acc)
+    f3 acc = mk(q.acc[0], q.acc[1], q.acc[2]);
+    Pcg32 g;
+    g.seed((uint64_t)(17 + p / W), (uint64_t)(23 + p % W));
+    g.skip(q.o);
+    for (uint32_t total = q.s; total < (uint32_t)spp; total++) acc = add(acc, sample(view, (int)p, g));
     b1::write_pixel(&img[(size_t)p * 3], acc, spp);
   }
   FILE *f = fopen(argv[5], "wb");
