@@ -1366,7 +1366,7 @@ static void launch_cost_pass(const rt_device_scene *d, b1::Book1View P, uint8_t 
   P.clean_col = (float4 *)d->ch_rec_arena;  // the previous chain launch's records back to kRecFill
   P.clean_n = d->ch_dirty;
   // at the chain kernel's occupancy, on its grid
-  // (the 3-wave instantiation, like the chain kernel's, spills nothing: N = 8 share pre-pass 4.3 ms at 5)
+  // (at the chain kernel's occupancy: the 3-wave instantiation for the shares; neither spills)
   const dim3 g((unsigned)d->chain_grid), blk(b1::kBlock);
   if (d->chain_occ == 3) {
     if (d->b1_lds_bytes) hipLaunchKernelGGL((rt_book1_cost_kernel<true, 3>), g, blk, d->b1_lds_bytes, st, P, d_out);
