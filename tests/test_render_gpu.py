@@ -252,7 +252,10 @@ def test_book1_deep_paths_spill(monkeypatch):
 
 @pytest.mark.parametrize("env", [{}, {"RT_CHAIN_BETA": "0.002"}, {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_KMAX": "64"},
                                  {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},
-                                 {"RT_CHAIN_OCC": "3"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"}])
+                                 {"RT_CHAIN_OCC": "3"}, {"RT_CHAIN_OCC": "5", "RT_CHAIN_BETA": "0.002"},
+                                 {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_COVER": "2", "RT_CHAIN_COVER_K": "2"},
+                                 {"RT_CHAIN_BETA": "0.002", "RT_CHAIN_OCC": "3", "RT_CHAIN_HEAVY": "3",
+                                  "RT_CHAIN_HEAVY_K": "2"}])
 def test_chain_render_north_star_scene(manifest, env, monkeypatch):
     """Chain render (rt_book1.h: ChainPx) forced on the Book-1 final scene at full size: pixel
     streams cut into segments, chains coupling on equal stream offsets, the fold and the
@@ -266,6 +269,34 @@ def test_chain_render_north_star_scene(manifest, env, monkeypatch):
     with rtc.use_diag():
         img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
     assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"], env
+
+
+def test_chain_record_arena_clean_across_launches(manifest, monkeypatch):
+    """The record arena is clean between chain launches only because each launch's cost pre-pass sets
+    the previous launch's reservation back (rt_book1.h: clean_records; no fill after the plan): launches
+    of shrinking and growing reservations on one device scene -- the whole frame, eight and two rank
+    shares, the whole frame again -- must each reproduce the reference rows."""
+    import torch
+
+    monkeypatch.setenv("RT_MODE", "chain")
+    monkeypatch.setenv("RT_LPT_SPP", "2")
+    monkeypatch.setenv("RT_CHAIN_MIN_SEG", "2")
+    monkeypatch.setenv("RT_CHAIN_BETA", "0.002")
+    e = manifest["renders"]["s1_300x168_16spp_d50"]
+    ref = golden_image(e)
+    with rtc.use_diag():
+        sc = rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"])
+        ds = rtc.DeviceScene(sc, 0)
+    stream = torch.cuda.current_stream(0)
+    for world, ranks in ((1, [0]), (8, range(8)), (2, range(2)), (1, [0]), (8, [7, 0])):
+        for rank in ranks:
+            row0, stride, n = rtc.rows_of(sc.height, rank, world)
+            buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+            ds.render_rows_async(row0, stride, n, buf.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            ds.check()
+            _check(buf.cpu().numpy(), ref[row0::stride][:n], f"chain launch rows {rank}/{world}")
+    ds.close()
 
 
 @pytest.mark.parametrize("env", [{"RT_GEN_BIG": "0"}, {"RT_GEN_BIG": "0", "RT_GEN_LDS": "0"},
