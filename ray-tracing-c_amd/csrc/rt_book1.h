@@ -182,6 +182,8 @@ struct Book1View {
   int32_t mig_live;
   uint32_t mig_epoch;  // per launch (> 0): marks the queue entries this launch wrote
   int32_t mig_idle;    // migrate only once more waves than this have become helpers
+  uint32_t walk_mask;  // a segment past its check looks for its pixel's end every walk_mask + 1 samples
+  uint32_t mig_poll;   // a sparse wave reads the helper count every this many ticks until the gate opens
   int32_t mig_sleep;     // helpers poll their mailbox every mig_sleep * ~3.4 us
   unsigned long long *loop_stats;  // diagnostic builds (-DRT_LOOP_STATS): per-launch loop counters
   int32_t mig_max_help;  // at most this many finished waves stay as helpers; the others leave.  Resident
@@ -747,7 +749,7 @@ RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_
     }
     return true;
   }
-  if (k > 0 && s >= P.check && (s & 3u) == 0u && chain_walk_done(V, P, k, s, spp)) {
+  if (k > 0 && s >= P.check && (s & V.walk_mask) == 0u && chain_walk_done(V, P, k, s, spp)) {
     if (writer) st_rel64(&V.ch_seg[P.end0 + k], end_word(s, false, 0u));
     return true;
   }
@@ -1195,8 +1197,10 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // migration: the work items are gone (a lane of this wave found none) and few lanes are left
     // and enough of the GPU idles (more than mig_idle waves have become helpers): before that,
     // whole-wave traces would take issue slots from lanes that still make full use of them.  The
-    // helper count is read at most every ~20 us per wave (a device-scope load per shading pass from
-    // every sparse wave measured 25 % slower lanes: one hot line).
+    // helper count is read at most every mig_poll ticks per wave (500 us): the device-scope load stalls
+    // the wave that needs its value (a load per shading pass from every sparse wave measured 25 % slower
+    // lanes; every 20 us, r02-r05a: N = 8 shares 58.7-59.2 ms against 56.0-57.2 at 500 us, N = 1 0.4 %;
+    // every 100 us from every dense wave as well: N = 8 +4 ms).
     // (Letting any drained wave migrate once 70-95 % of the waves had finished measured 8 % slower
     // at N = 8: whole-wave traces of dense waves' chains take the helpers from the sparse ones.)
     bool mig_try = false;
@@ -1205,7 +1209,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         const uint64_t now = wall_clock64();
         if (now >= mig_next) {
           mig_ok = (int32_t)ld_rel(&V.mig[kMigHelpers]) > V.mig_idle;  // (the count only grows)
-          mig_next = now + 2000u;
+          mig_next = now + V.mig_poll;
         }
       }
       mig_try = mig_ok;

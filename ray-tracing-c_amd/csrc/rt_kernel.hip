@@ -665,6 +665,10 @@ struct Config {
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
+  int mig_poll_us = 500;  //   a sparse wave's reads of the helper count until the gate opens (20 until r05:
+                         //   N = 8 58.7-59.2 vs 56.0-57.2 ms, same box; 100 / 1000 / 2000 between / equal)
+  int chain_walk = 4;  // a segment past its check walks its pixel's links every this many samples (power of
+                       // 2; 8 / 16 measured equal)
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
@@ -695,6 +699,9 @@ struct Config {
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
     c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
+    c.mig_poll_us = env_int("RT_MIG_POLL_US", c.mig_poll_us);
+    c.chain_walk = env_int("RT_CHAIN_WALK", c.chain_walk);
+    if (c.chain_walk < 1 || (c.chain_walk & (c.chain_walk - 1))) c.chain_walk = 4;
     c.mig_help = env_int("RT_MIG_HELP", c.mig_help);
     c.mig_sleep = env_int("RT_MIG_SLEEP", c.mig_sleep);
     if (c.mig_sleep < 1) c.mig_sleep = 1;
@@ -1526,6 +1533,8 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   V.coop_waves_dev = d->ch_cnt + kCnCoopWaves;
   V.mig_epoch = ++d->mig_epoch;
   V.mig_idle = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_idle / 100);
+  V.mig_poll = (uint32_t)(cfg.mig_poll_us > 1 ? cfg.mig_poll_us : 1) * 100u;
+  V.walk_mask = (uint32_t)(cfg.chain_walk > 1 ? cfg.chain_walk : 1) - 1u;
   V.mig_sleep = cfg.mig_sleep;
   V.mig_max_help = (int32_t)((int64_t)d->chain_grid * (b1::kBlock / 64) * cfg.mig_help / 100);
   V.mig_wait = (uint64_t)cfg.mig_wait_us * 100u;  // wall_clock64: 100 MHz

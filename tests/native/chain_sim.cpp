@@ -149,7 +149,7 @@ int main(int argc, char **argv) {
       chains.push_back(c);
     }
   }
-  col.assign(rec, make_float4(0, 0, 0, b1::u2f(b1::kRecFill)));  // (end word kRecFill: chain_fill_kernel)
+  col.assign(rec, make_float4(0, 0, 0, b1::u2f(b1::kRecFill)));  // (end word kRecFill: a clean arena)
   std::vector<uint32_t> mig(b1::kMigWords, 0u);
   b1::Book1View V;
   memset(&V, 0, sizeof V);
@@ -160,6 +160,7 @@ int main(int argc, char **argv) {
   V.ch_acc0 = acc0.data();
   V.mig = mig.data();
   V.mig_epoch = 1u;
+  V.walk_mask = 3u;  // (the product's default: a segment past its check walks every 4 samples)
   // interleaved execution: a random live chain takes one step (boundary, then one sample)
   std::vector<int> live;
   for (int c = 0; c < (int)chains.size(); c++) live.push_back(c);
