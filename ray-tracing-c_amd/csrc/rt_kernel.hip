@@ -265,18 +265,22 @@ constexpr size_t kLptHistBytes = 8192;
 // §5): the slowest lane chain's latency and the lanes' aggregate throughput per pre-pass traversal
 // step, and a whole-wave chain's rate.
 constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
-// Tail shaping (ChainModel.alpha) for launches at 3 waves per SIMD with at least kTailPx pixels per lane of
-// the 5-wave grid -- the N = 2 and N = 4 rank shares (1.24 and 0.62; N = 8: 0.31).  Same box, max rank ms,
-// three rounds: N = 2 alpha 0: 164.4-167.1, 1.5: 150.7-153.4, 2: 162.3-165.1, 3: 167.1-169.6;
-// N = 4 0: 94.0-95.3, 1.5: 93.5-94.5; N = 8 (two rounds) 0: 61.0-61.3, 1.5: 62.4-63.1; N = 1 (5 waves) 1.5:
-// 257.6-258.4 vs 252.0-252.8 ms per frame.
-constexpr float kTailAlpha3 = 1.5f, kTailPx = 0.5f;
-// Heavy pixels (ChainModel.heavy) at 3 waves per SIMD: a pixel planned at >= 8 lane segments gets twice as
-// many.  Its waves hold only heavy lanes (image-tile order) and run up to 3x slower per traversal step than
-// the planner's model (N = 8 rank 7: 0.45-0.70 ms per sample for 340-670 steps).  Same box,
-// N = 8 max rank ms, two rounds: off 60.9 / 60.5, 1.5: 60.7 / 59.7, 2: 59.7 / 59.4, 2 from 4 segments: 64.6 /
-// 64.1; N = 2 unchanged (147-148).
-constexpr float kHeavy3 = 2.0f;
+// Launch classes by pixels per lane of the 5-wave grid (pl; headline frame: N = 1 2.47, N = 2 1.24, N = 4 0.62,
+// N = 8 0.31): the one-GPU frame (pl >= chain_occ_px, 2), the N = 2 / 4 shares (kTailPx <= pl < 2) and the
+// N = 8 share (pl < kTailPx).  Since r05 every class runs the 5-wave kernel (the shares ran the 3-wave
+// instantiation since r03; same box, max rank ms, two rounds, each class at its best plan: 3 waves N = 2
+// 145.7 / 144.2, N = 4 87.9 / 89.5, N = 8 56.5 / 56.4; 5 waves 142.6 / 142.8, 85.3 / 85.7, 55.0 / 55.0).
+// Tail shaping (ChainModel.alpha) for the N = 2 / 4 shares.  Same box, max rank ms, three rounds, r05 at 3
+// waves: N = 2 alpha 0: 164.4-167.1, 1.5: 150.7-153.4, 2: 162.3-165.1, 3: 167.1-169.6; N = 4
+// 0: 94.0-95.3, 1.5: 93.5-94.5; N = 8 (two rounds) 0: 61.0-61.3, 1.5: 62.4-63.1 (5 waves: 60.1 / 60.0 vs
+// 55.0 / 55.0); N = 1 1.5: 257.6-258.4 vs 252.0-252.8 ms per frame.
+constexpr float kTailAlpha = 1.5f, kTailPx = 0.5f;
+// Heavy pixels (ChainModel.heavy) in the shares: a pixel planned at >= 8 lane segments gets twice as many.
+// Its waves hold only heavy lanes (image-tile order) and run up to 3x slower per traversal step than the
+// planner's model (N = 8 rank 7: 0.45-0.70 ms per sample for 340-670 steps).  Same box, N = 8
+// max rank ms, two rounds (3 waves): off 60.9 / 60.5, 1.5: 60.7 / 59.7, 2: 59.7 / 59.4, 2 from 4 segments:
+// 64.6 / 64.1; N = 2 unchanged (147-148).
+constexpr float kHeavy = 2.0f;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
@@ -667,6 +671,7 @@ struct Config {
   int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
   int mig_poll_us = 500;  //   a sparse wave's reads of the helper count until the gate opens (20 until r05:
                          //   N = 8 58.7-59.2 vs 56.0-57.2 ms, same box; 100 / 1000 / 2000 between / equal)
+  int chain_blocks3 = 0;  // (diagnostic) blocks per CU of the shares' chain kernel (0: as many as fit)
   int chain_walk = 4;  // a segment past its check walks its pixel's links every this many samples (power of
                        // 2; 8 / 16 measured equal)
   int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
@@ -677,11 +682,11 @@ struct Config {
   int cost_smooth = 4;     // planner cost = max(own, row mean +-cost_smooth) (cost_smooth_kernel; 0: own)
   int bucket_shift = 0;     // chain planner cost buckets merged 2^this at a time
   int tile_order = 32;      // > 0: chain items of one cost bucket grouped by image tiles this wide, 256 / it high (chain_scatter_kernel)
-  int chain_occ = 0;          // chain kernel waves per SIMD: 3, 5, or 0 = by pixels per lane (below)
-  float chain_occ_px = 2.0f;  //   auto: 5 when the launch has at least this many pixels per lane at 5,
-                              //   else 3 (headline frame: 2.47 at N = 1, 1.24 at N = 2 ... 0.31 at N = 8;
-                              //   same box, N = 1 / 2 / 4 / 8: 3 waves 268 / 168 / 100 / 68.5 ms, 4 waves
-                              //   274-277 / 172-180 / 102-104 / 69-70, 5 waves 265-267 / 172-177 / 105 / 70-73)
+  int chain_occ = 0;          // chain kernel waves per SIMD: 3 or 5 (0: 5; r03-r05a ran the shares at 3:
+                              //   same box, N = 1 / 2 / 4 / 8 with r03's plans: 3 waves 268 / 168 / 100 / 68.5 ms,
+                              //   4 waves 274-277 / 172-180 / 102-104 / 69-70, 5 waves 265-267 / 172-177 / 105 /
+                              //   70-73; with r05's plans 5 waves are ahead, kTailPx)
+  float chain_occ_px = 2.0f;  // launches of fewer pixels per lane of the 5-wave grid are rank shares (kTailPx)
   static Config from_env() {
     Config c;
     // the documented planner / scheduling parameters
@@ -751,6 +756,7 @@ struct Config {
     c.chain_pad_k = env_int("RT_CHAIN_PAD_K", c.chain_pad_k);
     c.chain_fill = env_float("RT_CHAIN_FILL", c.chain_fill);
     c.chain_occ_px = env_float("RT_CHAIN_OCC_PX", c.chain_occ_px);
+    c.chain_blocks3 = env_int("RT_CHAIN_BLOCKS3", c.chain_blocks3);
     c.chain_slack = env_int("RT_CHAIN_SLACK", c.chain_slack);  // (tests: tiny lists force continuations)
     if (c.chain_slack < 1) c.chain_slack = 1;
     c.gen_batch = env_int("RT_GEN_BATCH", c.gen_batch);
@@ -1065,6 +1071,10 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   d->b1_grid = prop.multiProcessorCount * (per_cu < 1 ? 1 : per_cu);
   d->chain_grid5 = prop.multiProcessorCount * (per_cu_chain < 1 ? 1 : per_cu_chain);
   d->chain_grid3 = prop.multiProcessorCount * (per_cu_chain3 < 1 ? 1 : per_cu_chain3);
+#ifdef RT_DIAG
+  if (cfg.chain_blocks3 > 0 && cfg.chain_blocks3 < per_cu_chain3)  // (A/B: fewer waves per SIMD for the shares)
+    d->chain_grid3 = prop.multiProcessorCount * cfg.chain_blocks3;
+#endif
   d->chain_grid = d->chain_grid5;
   const int chain_max = d->chain_grid5 > d->chain_grid3 ? d->chain_grid5 : d->chain_grid3;
   const int spill_grid = d->b1_grid > chain_max ? d->b1_grid : chain_max;
@@ -1424,9 +1434,8 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp, hipStream_t s
 // waves), the fold, and a continuation launch for whatever the fold could not finish.  No host sync.
 // The chain kernel's waves per SIMD for a launch of npix pixels (RT_CHAIN_OCC, else by pixels per lane).
 static int chain_occupancy(const rt_device_scene *d, int64_t npix) {
-  const int occ = d->cfg.chain_occ;
-  if (occ == 3 || occ == 5) return occ;
-  return (double)npix >= d->cfg.chain_occ_px * (double)d->chain_grid5 * b1::kBlock ? 5 : 3;
+  (void)npix;  // (every launch class at 5 since r05: the kTailPx note)
+  return d->cfg.chain_occ == 3 ? 3 : 5;
 }
 
 // A launch's bracket: the ev_main event (rt_scene_last_launch_ms) and a device timestamp in the
@@ -1472,9 +1481,11 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.lat = kLaneLat;
   m.thr = kLaneThr;
   m.coop = kCoopStep;
-  m.beta = cfg.chain_beta > 0.0f ? cfg.chain_beta : (d->chain_occ == 5 ? 0.9f : 0.7f);
-  m.alpha = cfg.chain_alpha >= 0.0f ? cfg.chain_alpha
-            : d->chain_occ == 3 && (double)npix >= kTailPx * (double)d->chain_grid5 * b1::kBlock ? kTailAlpha3 : 0.0f;
+  // the launch's class (kTailPx above): pixels per lane of the 5-wave grid
+  const double px_lane = (double)npix / ((double)d->chain_grid5 * b1::kBlock);
+  const bool share = px_lane < (double)cfg.chain_occ_px, mid_share = share && px_lane >= (double)kTailPx;
+  m.beta = cfg.chain_beta > 0.0f ? cfg.chain_beta : (mid_share ? 0.7f : 0.9f);
+  m.alpha = cfg.chain_alpha >= 0.0f ? cfg.chain_alpha : (mid_share ? kTailAlpha : 0.0f);
   m.floor = cfg.chain_floor;
   m.margin = cfg.chain_margin;
   m.slack = cfg.chain_slack;
@@ -1484,7 +1495,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.pad = cfg.chain_pad;
   m.cover = cfg.chain_cover;
   m.cover_k = cfg.chain_cover_k < 2 ? 2 : cfg.chain_cover_k;
-  m.heavy = cfg.chain_heavy >= 1.0f ? cfg.chain_heavy : (d->chain_occ == 3 ? kHeavy3 : 1.0f);
+  m.heavy = cfg.chain_heavy >= 1.0f ? cfg.chain_heavy : (share ? kHeavy : 1.0f);
   m.heavy_k = cfg.chain_heavy_k < 2 ? 2 : cfg.chain_heavy_k;
   m.pad_k = cfg.chain_pad_k < 2 ? 2 : cfg.chain_pad_k;
   m.kmax_lane = cfg.chain_kmax;
