@@ -668,7 +668,9 @@ struct Config {
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
-  int mig_idle = 50;  //   ... once this percentage of the grid's waves has finished
+  int mig_idle = 70;  //   ... once this percentage of the grid's waves has finished (50 until r05: same box, three
+                      //   rounds, N = 1 frame kernel p50 230.3-231.9 ms at 70 vs 231.8-232.8; N = 2 142.0 / 142.1
+                      //   vs 143.4 / 143.7, N = 8 equal; 85-90 slower)
   int mig_poll_us = 500;  //   a sparse wave's reads of the helper count until the gate opens (20 until r05:
                          //   N = 8 58.7-59.2 vs 56.0-57.2 ms, same box; 100 / 1000 / 2000 between / equal)
   int chain_blocks3 = 0;  // (diagnostic) blocks per CU of the shares' chain kernel (0: as many as fit)
