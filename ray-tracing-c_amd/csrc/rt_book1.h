@@ -163,6 +163,8 @@ struct Book1View {
   uint64_t *spill;           // [chunk][global lane]: a deep path's older 4-id chunks (Record)
   int32_t spill_lanes;
   int32_t n_bf_leaves;       // whole-wave pixels: leaves for bf_candidate; 0: off (coop_trace9 instead)
+  const struct BfCut *bf_cuts;  // and its subtree cuts (bf_candidate_cut); n_bf_cuts 0: every leaf each ray
+  int32_t n_bf_cuts;
   uint32_t *px_time;         // diagnostic (RT_PX_TIME=1): per work item {start, end, migrated}, wall_clock64 low bits
   // chain render (kMode 2)
   const ChainPx *ch_px;      // per pixel
@@ -561,6 +563,18 @@ RT_D void coop_trace9(const Book1View &V, const float4 *items, const CoopRay &C,
 // (r*, p*), p* = -1 for a miss; bf_verify is the ancestor check of a candidate p* >= 0.
 constexpr int kBfSlots = 8;  // 64 x 8 = 512 leaves at most (host-checked)
 
+// Subtree cuts for the candidate trace (host: book1_pack): at most 64 subtrees that partition the leaves,
+// each its root item q, its leaves [l0, l1) in preorder numbering and the node items enclosing q.  A
+// subtree whose root box is not entered at t_max = +inf is never entered (the test is monotone in t_max:
+// fminf(t, X) <= fminf(inf, X)), so none of its spheres is visited and none can be the reference's hit:
+// the candidate trace evaluates the roots of the entered subtrees' spheres only, one per lane, and the
+// ancestor check walks the cut's list and the cut's own subtree before the candidate.
+constexpr int kBfAnc = 12;
+struct BfCut {
+  uint16_t q, l0, l1, n_anc;
+  uint16_t anc[kBfAnc];
+};
+
 RT_D bool bf_candidate(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
                        int &out_bp) {
   const int lane = __lane_id();
@@ -598,6 +612,99 @@ RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, f
   const int lane = __lane_id();
   bool bad = false;
   for (int base = 0; base < bp; base += 64) {  // wave-uniform bound
+    const int q = base + lane;
+    if (q < bp) {
+      const float4 q1 = it_q1(items, na, q);
+      const uint32_t w = __float_as_uint(q1.w);
+      if (!(w & kLeaf9) && (uint32_t)bp < (uint32_t)q + __float_as_uint(q1.z)) {  // an ancestor of p*
+        float e, x;
+        box_interval(it_q0(items, q), q1, C, tmin, e, x);
+        bad |= !(fminf(best, x) > e);
+      }
+    }
+  }
+  return __ballot(bad) == 0;
+}
+
+// bf_candidate on the entered subtrees only (BfCut above); cut = the candidate's subtree (for bf_verify_cut).
+RT_D bool bf_candidate_cut(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
+                           int &out_bp, int &out_cut) {
+  const int lane = __lane_id();
+  const bool has = lane < V.n_bf_cuts;
+  uint32_t l0 = 0, cnt = 0;
+  if (has) {
+    const BfCut &K = V.bf_cuts[lane];
+    const float4 q1 = it_q1(items, V.n_items9_alloc, K.q);
+    bool in = true;  // a single sphere: always a candidate
+    if (!(__float_as_uint(q1.w) & kLeaf9)) {
+      float e, x;
+      box_interval(it_q0(items, K.q), q1, C, tmin, e, x);
+      in = !(fminf(__builtin_inff(), x) <= e);
+    }
+    l0 = K.l0;
+    cnt = in ? (uint32_t)(K.l1 - K.l0) : 0u;
+  }
+  uint32_t incl = cnt;  // inclusive prefix sum over the lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, off);
+    if (lane >= off) incl += t;
+  }
+  const uint32_t excl = incl - cnt;
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  float best = __builtin_inff();
+  int bp = 0x7fffffff, bc = -1;
+  bool nan = false;
+  for (uint32_t base = 0; base < total; base += 64) {  // wave-uniform
+    const uint32_t g = base + (uint32_t)lane;
+    // the lane's subtree: the last one whose exclusive prefix is <= g (empty ones share their successor's)
+    // (every lane takes part in every shuffle: a bpermute from a lane that is not executing it reads
+    // nothing)
+    int c = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+      const uint32_t v = (uint32_t)__shfl((int)excl, min(c + step, 63));
+      if (c + step < 64 && v <= g) c += step;
+    }
+    const bool live = g < total;
+    const uint32_t cl0 = (uint32_t)__shfl((int)l0, c), cex = (uint32_t)__shfl((int)excl, c);
+    const int n = live ? (int)(cl0 + (g - cex)) : 0;
+    const float4 h = it_q1(items, V.n_items9_alloc, n);
+    const uint32_t hw = __float_as_uint(h.w);
+    const int pos = (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw);
+    const float r = coop_sphere_root(it_q0(items, pos), C, tmin);
+    nan |= live && r != r;
+    if (live && r > tmin && (r < best || (r == best && pos < bp))) best = r, bp = pos, bc = c;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {  // argmin over (root, preorder position)
+    const float ob = __shfl_xor(best, off);
+    const int op = __shfl_xor(bp, off), oc = __shfl_xor(bc, off);
+    if (ob < best || (ob == best && op < bp)) best = ob, bp = op, bc = oc;
+  }
+  if (__ballot(nan) != 0) return false;
+  out_best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(best)));
+  bp = __builtin_amdgcn_readfirstlane(bp);
+  out_cut = __builtin_amdgcn_readfirstlane(bc);
+  out_bp = bp == 0x7fffffff ? -1 : bp;  // no valid root in any entered subtree: a miss
+  return true;
+}
+
+// bf_verify for a candidate of subtree cut: its ancestors are the cut's list and the nodes of the cut's
+// own subtree (its root included) that enclose bp.
+RT_D bool bf_verify_cut(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float best, int bp,
+                        int cut) {
+  const int lane = __lane_id();
+  const int na = V.n_items9_alloc;
+  const BfCut &K = V.bf_cuts[cut];
+  bool bad = false;
+  if (lane < (int)K.n_anc) {
+    const int q = K.anc[lane];
+    float e, x;
+    box_interval(it_q0(items, q), it_q1(items, na, q), C, tmin, e, x);
+    bad = !(fminf(best, x) > e);
+  }
+  for (int base = K.q; base < bp; base += 64) {  // wave-uniform bound
     const int q = base + lane;
     if (q < bp) {
       const float4 q1 = it_q1(items, na, q);
@@ -842,8 +949,9 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       C.fast = C.a >= kDivLo && C.a <= kDivHi;
       C.ra = recip_core(C.a);
       float tmax = __builtin_inff();
-      int bp = -1;
-      bool decided = use_bf && bf_candidate(V, items9, C, tmin, tmax, bp);
+      int bp = -1, cut = -1;
+      bool decided = use_bf && (V.n_bf_cuts > 0 ? bf_candidate_cut(V, items9, C, tmin, tmax, bp, cut)
+                                                : bf_candidate(V, items9, C, tmin, tmax, bp));
       // the hit sphere (center, 1/r, material) from its LDS item, and its material's load issued
       // before the ancestor check so that its latency overlaps it
       float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
@@ -851,7 +959,8 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       if (decided && bp >= 0) {
         s0 = it_q0(items9, bp), s1 = it_q1(items9, V.n_items9_alloc, bp);
         m = V.mats[__float_as_int(s1.z)];
-        decided = bf_verify(items9, V.n_items9_alloc, C, tmin, tmax, bp);
+        decided = V.n_bf_cuts > 0 ? bf_verify_cut(V, items9, C, tmin, tmax, bp, cut)
+                                  : bf_verify(items9, V.n_items9_alloc, C, tmin, tmax, bp);
       }
       if (!decided) {  // the exact scan
         int hit;

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -649,7 +650,7 @@ enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 // planner / scheduling parameters only; the diagnostic build (-DRT_DIAG) also the A/B switches.
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
-  bool lpt = true, bf = true, px_time = false, debug = false;
+  bool lpt = true, bf = true, bf_cuts = true, px_time = false, debug = false;
   bool pre_resume = true;     // chain items go on from the cost pre-pass's samples (RT_PRE_RESUME=0: off)
   int lpt_spp = 16, shade_batch = 48;
   // the chain launch's cost pre-pass spp (capped at a quarter of the frame's; lpt_spp is the least a chain
@@ -750,6 +751,7 @@ struct Config {
     c.lpt = env_flag("RT_LPT", true);
     c.pre_resume = env_flag("RT_PRE_RESUME", true);
     c.bf = env_flag("RT_BF", true);
+    c.bf_cuts = env_flag("RT_BF_CUTS", true);
     c.px_time = env_flag("RT_PX_TIME", false);
     c.debug = env_flag("RT_DEBUG", false);
     c.shade_batch = env_int("RT_SHADE_BATCH", c.shade_batch);
@@ -815,6 +817,7 @@ struct rt_device_scene {
   bool book1 = false;
   b1::Book1View b1view;
   void *b1_arena = nullptr;
+  b1::BfCut *bf_cuts = nullptr;  // the candidate trace's subtree cuts
   size_t b1_lds_bytes = 0;
   int b1_grid = 0, chain_grid = 0;  // chain_grid: the current chain launch's (one of the two below)
   int chain_grid5 = 0, chain_grid3 = 0, chain_occ = 5;  // chain kernel grids at 5 / 3 waves per SIMD
@@ -952,6 +955,7 @@ struct HostPack {
   bool book1 = false;
   std::vector<float4> items9;     // Book-1: the world in traversal preorder (rt_book1.h: trav_step_v9)
   int n_bf = 0;                   // leaves for the whole-wave candidate trace (0: off)
+  std::vector<b1::BfCut> bf_cuts; // and its subtree cuts (empty: every leaf each ray)
   std::vector<b1::FastMat> mats;
   std::vector<float4> pre;        // general path preorder (rt_device.h: build_preorder)
 };
@@ -1030,6 +1034,47 @@ static void book1_pack(const rt_flat_scene *s, HostPack &H) {
       h.w = bits_as_float(bf_item[n]);
   }
   H.n_bf = !bf_item.empty() && bf_item.size() <= (size_t)64 * b1::kBfSlots && H.cfg.bf ? (int)bf_item.size() : 0;
+  // subtree cuts for the candidate trace (rt_book1.h: BfCut): from the top-level items, split the cut of most
+  // leaves into its children while at most 64 cuts result and a cut holds more than 4 leaves
+  if (H.n_bf > 0 && H.cfg.bf_cuts) {
+    const int n = (int)(items9.size() / 2) - 1;  // (without the pad item)
+    auto word = [&](int q, int c) { uint32_t w; memcpy(&w, (const char *)&items9[2 * q + 1] + 4 * c, 4); return w; };
+    auto leaf = [&](int q) { return (word(q, 3) & b1::kLeaf9) != 0; };
+    auto size_of = [&](int q) { return leaf(q) ? 1 : (int)word(q, 2); };
+    std::vector<int> lb((size_t)n + 1, 0);  // leaves before item q (the candidate trace's numbering)
+    for (int q = 0; q < n; q++) lb[q + 1] = lb[q] + (leaf(q) ? 1 : 0);
+    std::vector<int> cuts;
+    for (int q = 0; q < n; q += size_of(q)) cuts.push_back(q);
+    auto leaves = [&](int q) { return lb[q + size_of(q)] - lb[q]; };
+    bool ok = !cuts.empty() && cuts.size() <= 64 && lb[n] == H.n_bf;
+    while (ok) {
+      int at = -1;
+      for (size_t k = 0; k < cuts.size(); k++)
+        if (!leaf(cuts[k]) && (at < 0 || leaves(cuts[k]) > leaves(cuts[at]))) at = (int)k;
+      if (at < 0 || leaves(cuts[at]) <= 4) break;
+      const int q = cuts[at];
+      std::vector<int> kids;
+      for (int c = q + 1; c < q + size_of(q); c += size_of(c)) kids.push_back(c);
+      if (cuts.size() - 1 + kids.size() > 64) break;
+      cuts.erase(cuts.begin() + at);
+      cuts.insert(cuts.end(), kids.begin(), kids.end());
+    }
+    std::sort(cuts.begin(), cuts.end());
+    for (size_t k = 0; ok && k < cuts.size(); k++) {
+      b1::BfCut c;
+      memset(&c, 0, sizeof c);
+      const int q = cuts[k];
+      c.q = (uint16_t)q, c.l0 = (uint16_t)lb[q], c.l1 = (uint16_t)lb[q + size_of(q)];
+      for (int a = 0; a < q && ok; a++)
+        if (!leaf(a) && a + size_of(a) > q) {
+          if (c.n_anc >= b1::kBfAnc) ok = false;
+          else c.anc[c.n_anc++] = (uint16_t)a;
+        }
+      ok = ok && n < 65535;
+      H.bf_cuts.push_back(c);
+    }
+    if (!ok) H.bf_cuts.clear();
+  }
   H.mats.resize(s->n_materials);
   for (int k = 0; k < s->n_materials; k++) {
     const rt_material &m = s->materials[k];
@@ -1143,6 +1188,12 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.spill_lanes = spill_lanes;
   V.shade_batch = cfg.shade_batch;
   V.n_bf_leaves = H.n_bf;
+  if (!H.bf_cuts.empty()) {
+    HIP_OK(hipMalloc(&d->bf_cuts, H.bf_cuts.size() * sizeof(b1::BfCut)));
+    HIP_OK(hipMemcpy(d->bf_cuts, H.bf_cuts.data(), H.bf_cuts.size() * sizeof(b1::BfCut), hipMemcpyHostToDevice));
+    V.bf_cuts = d->bf_cuts;
+    V.n_bf_cuts = (int32_t)H.bf_cuts.size();
+  }
   d->lpt_cost = (uint32_t *)(b + off[4]);
   d->lpt_order = (int32_t *)(b + off[5]);
   d->lpt_hist = (uint32_t *)(b + off[6]);
@@ -1362,6 +1413,7 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->launched && d->ev_done) (void)hipEventSynchronize(d->ev_done);  // no launch of this scene in flight
   (void)hipFree(d->arena);
   if (d->b1_arena) (void)hipFree(d->b1_arena);
+  if (d->bf_cuts) (void)hipFree(d->bf_cuts);
   if (d->gen_arena) (void)hipFree(d->gen_arena);
   if (d->gen_xrec) (void)hipFree(d->gen_xrec);
   if (d->gen_pre) (void)hipFree(d->gen_pre);
