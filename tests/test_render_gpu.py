@@ -219,6 +219,8 @@ SPLIT = {**CHAIN, "RT_CHAIN_BETA": "0.001"}  # every pixel split as far as allow
     {**SPLIT, "RT_BOOK1_LDS": "0"},                           #   ... chain render on them (lanes only)
     CHAIN, SPLIT,                                             # the chain render, planned / fully split
     {**SPLIT, "RT_CHAIN_KMAX": "1"},                          # every split pixel on whole waves
+    {**SPLIT, "RT_CHAIN_KMAX": "1", "RT_BF_CUTS": "0"},       #   ... their candidate trace over every leaf
+    {**SPLIT, "RT_CHAIN_KMAX": "1", "RT_BF": "0"},            #   ... and the exact whole-wave scan
     {**SPLIT, "RT_CHAIN_MARGIN": "1.0", "RT_CHAIN_SLACK": "1"},  # lists that fill up: continuations
     {**SPLIT, "RT_CHAIN_MB": "1"},                            # out of records: pixels stay whole
     {**CHAIN, "RT_CHAIN_OCC": "3"}, {**CHAIN, "RT_CHAIN_OCC": "5"},  # both chain kernel occupancies
