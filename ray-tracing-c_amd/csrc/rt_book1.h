@@ -91,6 +91,7 @@ struct ChainCont {     // 32 B: a continuation item -- the true chain from an ex
 constexpr int kMigBoxes = 64, kMigBoxWords = 32;
 enum : int {
   kMigDone = 0, kMigHelpers = 1, kMigDropped = 2, kMigBox0 = 64,
+  kMigStat = 4,  // (diagnostic build, RT_DEBUG: 6 u64 of migrated items' rays and clocks, words 4-15)
   kMigPush = 0, kMigPop = 1, kMigCredits = 2, kMigFinished = 3
 };
 constexpr int kMigWords = kMigBox0 + kMigBoxes * kMigBoxWords;
@@ -626,6 +627,44 @@ RT_D bool bf_verify(const float4 *items, int na, const CoopRay &C, float tmin, f
   return __ballot(bad) == 0;
 }
 
+// Wave scans on DPP (row shifts within 16-lane rows, then the gfx9 row broadcasts of lanes 15 and 31)
+// instead of ds_bpermute: a step is a VALU move, not an LDS-crossbar round trip.  Every lane must be
+// active.  Lanes without a source keep `old`, the operation's identity.
+constexpr int kDppRowShr = 0x110, kDppBcast15 = 0x142, kDppBcast31 = 0x143;
+template <int kCtrl, int kRows>
+RT_D uint32_t dpp_mov(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kCtrl, kRows, 0xf, false);
+}
+template <int kCtrl, int kRows>
+RT_D void dpp_sum_step(uint32_t &x) { x += dpp_mov<kCtrl, kRows>(0u, x); }
+RT_D uint32_t wave_incl_sum(uint32_t x) {  // inclusive prefix sum over the lanes
+  dpp_sum_step<kDppRowShr + 1, 0xf>(x);
+  dpp_sum_step<kDppRowShr + 2, 0xf>(x);
+  dpp_sum_step<kDppRowShr + 4, 0xf>(x);
+  dpp_sum_step<kDppRowShr + 8, 0xf>(x);
+  dpp_sum_step<kDppBcast15, 0xa>(x);  // rows 1, 3 += lane 15 / 47
+  dpp_sum_step<kDppBcast31, 0xc>(x);  // rows 2, 3 += lane 31
+  return x;
+}
+template <int kCtrl, int kRows>
+RT_D void dpp_min_step(uint64_t &k) {
+  const uint32_t lo = dpp_mov<kCtrl, kRows>(0xffffffffu, (uint32_t)k);
+  const uint32_t hi = dpp_mov<kCtrl, kRows>(0xffffffffu, (uint32_t)(k >> 32));
+  const uint64_t o = (uint64_t)hi << 32 | lo;
+  k = o < k ? o : k;
+}
+RT_D uint64_t wave_min_u64(uint64_t k) {  // the least key of the wave (wave-uniform)
+  dpp_min_step<kDppRowShr + 1, 0xf>(k);
+  dpp_min_step<kDppRowShr + 2, 0xf>(k);
+  dpp_min_step<kDppRowShr + 4, 0xf>(k);
+  dpp_min_step<kDppRowShr + 8, 0xf>(k);
+  dpp_min_step<kDppBcast15, 0xa>(k);
+  dpp_min_step<kDppBcast31, 0xc>(k);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), 63);
+  return (uint64_t)hi << 32 | lo;
+}
+
 // bf_candidate on the entered subtrees only (BfCut above); cut = the candidate's subtree (for bf_verify_cut).
 RT_D bool bf_candidate_cut(const Book1View &V, const float4 *items, const CoopRay &C, float tmin, float &out_best,
                            int &out_bp, int &out_cut) {
@@ -644,12 +683,7 @@ RT_D bool bf_candidate_cut(const Book1View &V, const float4 *items, const CoopRa
     l0 = K.l0;
     cnt = in ? (uint32_t)(K.l1 - K.l0) : 0u;
   }
-  uint32_t incl = cnt;  // inclusive prefix sum over the lanes
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)incl, off);
-    if (lane >= off) incl += t;
-  }
+  const uint32_t incl = wave_incl_sum(cnt);
   const uint32_t excl = incl - cnt;
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   float best = __builtin_inff();
@@ -676,16 +710,14 @@ RT_D bool bf_candidate_cut(const Book1View &V, const float4 *items, const CoopRa
     nan |= live && r != r;
     if (live && r > tmin && (r < best || (r == best && pos < bp))) best = r, bp = pos, bc = c;
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {  // argmin over (root, preorder position)
-    const float ob = __shfl_xor(best, off);
-    const int op = __shfl_xor(bp, off), oc = __shfl_xor(bc, off);
-    if (ob < best || (ob == best && op < bp)) best = ob, bp = op, bc = oc;
-  }
+  // argmin over (root, preorder position): a valid root is > t_min > 0, so its bits order as the floats
+  const uint64_t key = (uint64_t)__float_as_uint(best) << 32 | (uint32_t)bp;
+  const uint64_t win = wave_min_u64(key);
   if (__ballot(nan) != 0) return false;
-  out_best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(best)));
-  bp = __builtin_amdgcn_readfirstlane(bp);
-  out_cut = __builtin_amdgcn_readfirstlane(bc);
+  const int wl = __builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)__ballot(key == win)) - 1);
+  out_best = __uint_as_float((uint32_t)(win >> 32));
+  bp = (int)(uint32_t)win;
+  out_cut = __builtin_amdgcn_readlane(bc, wl);
   out_bp = bp == 0x7fffffff ? -1 : bp;  // no valid root in any entered subtree: a miss
   return true;
 }
@@ -912,6 +944,12 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
   const bool use_bf = V.n_bf_leaves > 0;
   const uint32_t px_start = V.px_time && !res ? (uint32_t)wall_clock64() : 0u;
   if (kMode == 2 && V.px_time && lane0 && !res) chain_time(V, pix, seg, 0);
+#ifdef RT_DIAG
+  // (diagnostic: a migrated item's rays, exact scans, and shader clocks in the candidate trace, the
+  // ancestor check, the exact scans and the whole item)
+  uint64_t d_ray = 0, d_exact = 0, d_cand = 0, d_ver = 0, d_scan = 0;
+  const uint64_t d_t0 = clock64();
+#endif
   for (;;) {
     if (kMode == 2) {  // (wave-uniform: every lane loads the same words; lane 0's view decides)
       const bool done = chain_boundary(V, pix, seg, g.n, s, acc, tc, st, out, lane0);
@@ -950,8 +988,15 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
       C.ra = recip_core(C.a);
       float tmax = __builtin_inff();
       int bp = -1, cut = -1;
+#ifdef RT_DIAG
+      const uint64_t d_a = clock64();
+#endif
       bool decided = use_bf && (V.n_bf_cuts > 0 ? bf_candidate_cut(V, items9, C, tmin, tmax, bp, cut)
                                                 : bf_candidate(V, items9, C, tmin, tmax, bp));
+#ifdef RT_DIAG
+      const uint64_t d_b = clock64();
+      d_cand += d_b - d_a, d_ray++;
+#endif
       // the hit sphere (center, 1/r, material) from its LDS item, and its material's load issued
       // before the ancestor check so that its latency overlaps it
       float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
@@ -961,10 +1006,19 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
         m = V.mats[__float_as_int(s1.z)];
         decided = V.n_bf_cuts > 0 ? bf_verify_cut(V, items9, C, tmin, tmax, bp, cut)
                                   : bf_verify(items9, V.n_items9_alloc, C, tmin, tmax, bp);
+#ifdef RT_DIAG
+        d_ver += clock64() - d_b;
+#endif
       }
       if (!decided) {  // the exact scan
         int hit;
+#ifdef RT_DIAG
+        const uint64_t d_c = clock64();
+#endif
         coop_trace9(V, items9, C, tmin, tmax, hit);
+#ifdef RT_DIAG
+        d_scan += clock64() - d_c, d_exact++;
+#endif
         bp = hit;
         if (hit >= 0) {
           const rt_sphere &sp = V.S.spheres[hit];
@@ -1000,6 +1054,14 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
     }
     s++;
   }
+#ifdef RT_DIAG
+  if (res && V.px_time && lane0) {
+    unsigned long long *st = (unsigned long long *)(V.mig + kMigStat);
+    atomicAdd(st + 0, (unsigned long long)d_ray), atomicAdd(st + 1, (unsigned long long)d_exact);
+    atomicAdd(st + 2, (unsigned long long)d_cand), atomicAdd(st + 3, (unsigned long long)d_ver);
+    atomicAdd(st + 4, (unsigned long long)d_scan), atomicAdd(st + 5, (unsigned long long)(clock64() - d_t0));
+  }
+#endif
   if (kMode != 2 && lane0) write_pixel(out + pix * 3, acc, cam.spp);
   if (V.px_time && lane0 && kMode != 2) {
     if (!res) V.px_time[3 * pix] = px_start;

@@ -1646,6 +1646,12 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
       }
       fprintf(stderr, "[rtc] chain launch migration: helpers %u pushed %llu popped %llu done %u\n", mw[b1::kMigHelpers],
               (unsigned long long)pushed, (unsigned long long)popped, mw[b1::kMigDone]);
+      uint64_t ms[6];  // (diagnostic build with RT_PX_TIME: the migrated items' rays and shader clocks)
+      memcpy(ms, &mw[b1::kMigStat], sizeof(ms));
+      if (ms[0])
+        fprintf(stderr, "[rtc] migrated items: rays %llu exact scans %llu; clocks per ray: candidate %.0f ancestors %.0f "
+                "exact %.0f item %.0f\n", (unsigned long long)ms[0], (unsigned long long)ms[1], (double)ms[2] / ms[0],
+                (double)ms[3] / ms[0], (double)ms[4] / ms[0], (double)ms[5] / ms[0]);
     }
   }
   hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)(npix / 64 + 1 < 8192 ? npix / 64 + 1 : 8192)), dim3(64), 0, st,
