@@ -647,6 +647,20 @@ RT_D uint32_t wave_incl_sum(uint32_t x) {  // inclusive prefix sum over the lane
   return x;
 }
 template <int kCtrl, int kRows>
+RT_D void dpp_max_step(uint32_t &x) {
+  const uint32_t o = dpp_mov<kCtrl, kRows>(0u, x);
+  x = o > x ? o : x;
+}
+RT_D uint32_t wave_incl_max(uint32_t x) {  // inclusive prefix max over the lanes
+  dpp_max_step<kDppRowShr + 1, 0xf>(x);
+  dpp_max_step<kDppRowShr + 2, 0xf>(x);
+  dpp_max_step<kDppRowShr + 4, 0xf>(x);
+  dpp_max_step<kDppRowShr + 8, 0xf>(x);
+  dpp_max_step<kDppBcast15, 0xa>(x);
+  dpp_max_step<kDppBcast31, 0xc>(x);
+  return x;
+}
+template <int kCtrl, int kRows>
 RT_D void dpp_min_step(uint64_t &k) {
   const uint32_t lo = dpp_mov<kCtrl, kRows>(0xffffffffu, (uint32_t)k);
   const uint32_t hi = dpp_mov<kCtrl, kRows>(0xffffffffu, (uint32_t)(k >> 32));
@@ -686,23 +700,32 @@ RT_D bool bf_candidate_cut(const Book1View &V, const float4 *items, const CoopRa
   const uint32_t incl = wave_incl_sum(cnt);
   const uint32_t excl = incl - cnt;
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  // a non-empty cut's key: its index and the offset from its compacted leaves to its leaf numbers
+  // (l0 >= excl: compaction only drops leaves), so that a lane's leaf is g + offset
+  const uint32_t ckey = (uint32_t)lane << 16 | (l0 - excl);
+  const uint64_t nonempty = __ballot(cnt > 0);
   float best = __builtin_inff();
   int bp = 0x7fffffff, bc = -1;
   bool nan = false;
   for (uint32_t base = 0; base < total; base += 64) {  // wave-uniform
     const uint32_t g = base + (uint32_t)lane;
-    // the lane's subtree: the last one whose exclusive prefix is <= g (empty ones share their successor's)
-    // (every lane takes part in every shuffle: a bpermute from a lane that is not executing it reads
-    // nothing)
-    int c = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-      const uint32_t v = (uint32_t)__shfl((int)excl, min(c + step, 63));
-      if (c + step < 64 && v <= g) c += step;
+    // the lane's subtree: the last non-empty one starting at or before g.  Its key is written to the lane
+    // where it starts (lane 0: the cut that holds `base`; a scalar loop over the cuts
+    // that start inside the window), then a prefix max hands every lane the last start before it (the
+    // keys grow with the start).
+    const uint64_t upto = nonempty & __ballot(excl <= base);  // (non-empty: holds the cut of excl 0)
+    const int c0 = 63 - (int)__builtin_clzll(upto);
+    uint32_t mark = lane == 0 ? (uint32_t)__builtin_amdgcn_readlane((int)ckey, c0) : 0u;
+    for (uint64_t st = nonempty & __ballot(excl > base && excl < base + 64u); st; st &= st - 1) {
+      const int c = (int)__builtin_ctzll(st);
+      const int at = __builtin_amdgcn_readlane((int)excl, c) - (int)base;
+      const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)ckey, c);
+      mark = lane == at ? kc : mark;
     }
+    const uint32_t k = wave_incl_max(mark);
+    const int c = (int)(k >> 16);
     const bool live = g < total;
-    const uint32_t cl0 = (uint32_t)__shfl((int)l0, c), cex = (uint32_t)__shfl((int)excl, c);
-    const int n = live ? (int)(cl0 + (g - cex)) : 0;
+    const int n = live ? (int)(g + (k & 0xffffu)) : 0;
     const float4 h = it_q1(items, V.n_items9_alloc, n);
     const uint32_t hw = __float_as_uint(h.w);
     const int pos = (int)((hw & kLeaf9) ? __float_as_uint(h.x) : hw);
