@@ -752,14 +752,21 @@ RT_D bool bf_verify_cut(const Book1View &V, const float4 *items, const CoopRay &
   const int lane = __lane_id();
   const int na = V.n_items9_alloc;
   const BfCut &K = V.bf_cuts[cut];
+  const int n_anc = K.n_anc;
   bool bad = false;
-  if (lane < (int)K.n_anc) {
-    const int q = K.anc[lane];
-    float e, x;
-    box_interval(it_q0(items, q), it_q1(items, na, q), C, tmin, e, x);
-    bad = !(fminf(best, x) > e);
+  {  // one pass: lanes [0, n_anc) the cut's ancestors, the lanes above them the cut's first items before bp
+    const int q = lane < n_anc ? (int)K.anc[lane] : (int)K.q + (lane - n_anc);
+    if (q < bp) {  // (an ancestor precedes bp)
+      const float4 q1 = it_q1(items, na, q);
+      const uint32_t w = __float_as_uint(q1.w);
+      if (lane < n_anc || (!(w & kLeaf9) && (uint32_t)bp < (uint32_t)q + __float_as_uint(q1.z))) {
+        float e, x;
+        box_interval(it_q0(items, q), q1, C, tmin, e, x);
+        bad = !(fminf(best, x) > e);
+      }
+    }
   }
-  for (int base = K.q; base < bp; base += 64) {  // wave-uniform bound
+  for (int base = (int)K.q + 64 - n_anc; base < bp; base += 64) {  // wave-uniform bound (rarely entered)
     const int q = base + lane;
     if (q < bp) {
       const float4 q1 = it_q1(items, na, q);
