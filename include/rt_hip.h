@@ -72,9 +72,29 @@ int rt_scene_check(rt_device_scene *dscene);
  * devices were visible (share g on device g % visible count). */
 int rt_render(const rt_flat_scene *scene, int n_gpus, uint8_t *out_host);
 
+/* One share of rt_render's partition, for a driver that runs one process (or thread) per GPU (bench.py
+ * under torchrun, the cgo / JNI drivers of INTEGRATION.md): rows j % n_shares == share on `device`,
+ * written into those rows of out_host (a whole frame's buffer, width*height*3; other rows untouched).
+ * Synchronous; 0 only when every pixel of the share was rendered.  Replaces the per-GPU slice of the
+ * reference's one `Camera_render` loop (src/raytracing.c:91-135), whose rows the reference's OpenMP
+ * team shares out within one process. */
+int rt_render_share(const rt_flat_scene *scene, int share, int n_shares, int device, uint8_t *out_host);
+
+/* rt_render and rt_render_share keep each share's device scene (arrays, plan scratch, the record arena),
+ * output rows and stream after the call, keyed by the scene's bytes, the partition and the RT_*
+ * environment: a repeated call with the same scene renders without upload or allocation (DESIGN.md
+ * §5.3).  One partition per device is kept; RT_SCENE_CACHE=0 keeps nothing.  This frees what is kept
+ * (call it before freeing device memory for other work; in-flight calls finish first). */
+void rt_render_cache_release(void);
+
 /* Kernel-side timing of the last rt_render call on `device`: milliseconds between HIP events
  * bracketing its kernel launches (excludes upload and D2H). */
 double rt_last_kernel_ms(int device);
+
+/* Host wall-clock phases of the last rt_render / rt_render_share of share `share` (ms[4]): setup
+ * (upload and allocations; ~0 when the cached scene was reused), launch to finish (pre-pass, plan,
+ * kernels), D2H of its rows with the completion check, and the whole call. */
+int rt_last_share_ms(int share, double *ms);
 
 /* Diagnostics: evaluate the device libm port (rt_libm.h) on n inputs.
  * fn: 0 = sincosf (out[2i] = sin, out[2i+1] = cos), 1 = powf(x, 5), 2 = logf, 3 = sinf,

@@ -21,6 +21,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstddef>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -601,13 +604,29 @@ __global__ __launch_bounds__(1024) void chain_wave_sort_kernel(const uint32_t *c
 }
 
 // The records this launch reserved (and may write), for the next launch's cost pre-pass to set back to
-// kRecFill (rt_book1.h: clean_records; the arena is clean when the launch starts).
+// kRecFill (rt_book1.h: clean_records).  The arena's records [0, hw) are clean when a launch starts; a
+// fresh arena has hw = 0 and is not filled when it is allocated (a 24-GiB memset per new arena cost the
+// drop-in path milliseconds per call: DESIGN.md §5.3): the records this launch reserves past hw are filled
+// by chain_fill_kernel right after the plan, [lo, hi) = [hw, max(hw, n)), and hw moves up to hi.
+// dirty[0]: the reservation (what the next pre-pass cleans), dirty[1]: hw, dirty[2..3]: this launch's fill.
+enum : int { kDirtyN = 0, kDirtyHw = 1, kDirtyLo = 2, kDirtyHi = 3, kDirtyWords = 4 };
 __global__ void chain_dirty_kernel(uint32_t *cnt, uint32_t *dirty, uint32_t cap) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const unsigned long long c = *(const unsigned long long *)&cnt[kCnRec];
   const uint32_t n = c < cap ? (uint32_t)c : cap;  // (the count includes reservations past the capacity)
   cnt[kCnFilled] = n;
-  *dirty = n;
+  const uint32_t hw = dirty[kDirtyHw], hi = n > hw ? n : hw;
+  dirty[kDirtyN] = n;
+  dirty[kDirtyLo] = hw;
+  dirty[kDirtyHi] = hi;
+  dirty[kDirtyHw] = hi;
+}
+// (records [lo, hi) to kRecFill; nothing to do -- every launch on a warm arena -- exits at once)
+__global__ __launch_bounds__(256) void chain_fill_kernel(float4 *col, const uint32_t *dirty) {
+  const uint64_t lo = dirty[kDirtyLo], hi = dirty[kDirtyHi];
+  const float4 fill = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(b1::kRecFill));
+  for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * blockDim.x)
+    col[i] = fill;
 }
 
 constexpr size_t kCounterBytes = 128 + b1::kMigWords * sizeof(uint32_t);  // work counter line + migration words
@@ -1223,7 +1242,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     char *c = (char *)d->ch_arena;
     d->ch_cnt = (uint32_t *)(c + co[0]);
     d->ch_dirty = d->ch_cnt + kCnWords;  // (past the words each plan zeroes)
-    HIP_OK(hipMemset(d->ch_dirty, 0, sizeof(uint32_t)));
+    HIP_OK(hipMemset(d->ch_dirty, 0, kDirtyWords * sizeof(uint32_t)));
     d->ch_k = (uint32_t *)(c + co[1]);
     d->ch_split = (uint32_t *)(c + co[2]);
     d->ch_px = (b1::ChainPx *)(c + co[3]);
@@ -1494,10 +1513,9 @@ static int chain_records(rt_device_scene *d, size_t npix, int spp, hipStream_t s
   d->ch_rec_cap = 0;
   HIP_OK(hipMalloc(&d->ch_rec_arena, want * sizeof(float4) + 256));
   d->ch_rec_cap = want;
-  // a fresh arena: every word kRecFill (0xff bytes; colours are read only from written records), and
+  // a fresh arena: nothing clean yet (hw 0: chain_fill_kernel fills what each launch reserves past hw),
   // nothing for the next pre-pass to set back
-  HIP_OK(hipMemsetAsync(d->ch_rec_arena, 0xff, want * sizeof(float4), st));
-  HIP_OK(hipMemsetAsync(d->ch_dirty, 0, sizeof(uint32_t), st));
+  HIP_OK(hipMemsetAsync(d->ch_dirty, 0, kDirtyWords * sizeof(uint32_t), st));
   return 0;
 }
 
@@ -1592,6 +1610,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
                      m.bucket_shift);
   hipLaunchKernelGGL(chain_wave_sort_kernel, dim3(1), dim3(1024), 0, st, d->ch_cnt, d->ch_items, d->ch_wave_key);
   hipLaunchKernelGGL(chain_dirty_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, d->ch_dirty, (uint32_t)d->ch_rec_cap);
+  hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, col, (const uint32_t *)d->ch_dirty);
   HIP_OK(hipGetLastError());
   if (cfg.debug) {  // diagnostic: synchronous peek at the plan
     uint32_t c[16];
@@ -1927,68 +1946,208 @@ extern "C" int rt_scene_check(rt_device_scene *d) {
                       "(status 0x%x); the frame is not valid", d->device, st[1], st[0]), -1;
 }
 
+// ------------------------------------------------------------------------------ device-scene cache
+// A share -- rows j % n_shares == share of a frame, on one device -- keeps its device scene (arrays, plan
+// scratch and the chain-record arena, which stays clean between launches), its output rows and its stream
+// after the call, keyed by every byte of the flat scene, the share, and the RT_* environment the scene's
+// Config is read from.  The next rt_render / rt_render_share with an identical key renders at once: a
+// driver that calls Camera_render frame after frame pays the upload, the allocations and the first
+// launch's record fill once.  One layout (key, n_shares) per device: a call with another
+// layout frees the device's idle slots first.  RT_SCENE_CACHE=0: nothing is kept (every call uploads and
+// frees); rt_render_cache_release() frees what is kept.
+struct ShareSlot {
+  int device = -1, share = -1, n_shares = 0;
+  std::string key;
+  rt_device_scene *scene = nullptr;
+  hipStream_t stream = nullptr;
+  uint8_t *d_out = nullptr;
+  bool busy = false, cached = false;
+};
+static std::mutex g_cache_mu;
+static std::vector<ShareSlot *> &cache_slots() {  // (never destroyed: no HIP call from a static destructor)
+  static std::vector<ShareSlot *> *v = new std::vector<ShareSlot *>();
+  return *v;
+}
+
+static void slot_free(ShareSlot *e) {
+  (void)hipSetDevice(e->device);
+  if (e->scene) rt_scene_release(e->scene);  // (waits for the scene's last launch)
+  if (e->d_out) (void)hipFree(e->d_out);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+extern char **environ;
+static std::string scene_key(const rt_flat_scene *s, int per_dev) {
+  std::string k;
+  auto add = [&k](const void *p, size_t n) {
+    if (p && n) k.append((const char *)p, n);
+  };
+  add(s, offsetof(rt_flat_scene, bvh));  // camera, root, lights, features, counts
+  add(s->bvh, sizeof(rt_bvh_node) * s->n_bvh);
+  add(s->spheres, sizeof(rt_sphere) * s->n_spheres);
+  add(s->quads, sizeof(rt_quad) * s->n_quads);
+  add(s->lists, sizeof(rt_list) * s->n_lists);
+  add(s->list_items, sizeof(int32_t) * s->n_list_items);
+  add(s->translates, sizeof(rt_translate) * s->n_translates);
+  add(s->rotates, sizeof(rt_rotate_y) * s->n_rotates);
+  add(s->media, sizeof(rt_medium) * s->n_media);
+  add(s->materials, sizeof(rt_material) * s->n_materials);
+  add(s->textures, sizeof(rt_texture) * s->n_textures);
+  add(s->images, sizeof(rt_image) * s->n_images);
+  add(s->perlins, sizeof(rt_perlin) * s->n_perlins);
+  add(s->image_bytes, (size_t)s->n_image_bytes);
+  std::vector<std::string> env;
+  for (char **e = environ; e && *e; e++)
+    if (!strncmp(*e, "RT_", 3)) env.emplace_back(*e);
+  std::sort(env.begin(), env.end());
+  for (const std::string &e : env) k.append(e).push_back('\0');
+  add(&per_dev, sizeof per_dev);
+  return k;
+}
+
+// A slot for (device, share, n_shares): the cached one when its key matches and no other call holds it,
+// else a new one (cached when the cache is on and no identical slot is in use).
+static ShareSlot *slot_acquire(const std::string *key, int device, int share, int n_shares) {
+  std::vector<ShareSlot *> stale;
+  ShareSlot *e = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    std::vector<ShareSlot *> &v = cache_slots();
+    bool in_use = false;
+    for (size_t i = 0; i < v.size();) {
+      ShareSlot *c = v[i];
+      const bool same = key && c->n_shares == n_shares && c->key == *key;
+      if (c->device == device && same && c->share == share) {
+        if (!c->busy) e = c, e->busy = true;
+        else in_use = true;
+      }
+      if (c->device == device && !same && !c->busy) {  // another layout on this device: freed
+        stale.push_back(c);
+        v.erase(v.begin() + (ptrdiff_t)i);
+        continue;
+      }
+      i++;
+    }
+    if (!e) {
+      e = new ShareSlot();
+      e->device = device, e->share = share, e->n_shares = n_shares, e->busy = true;
+      if (key && !in_use) e->key = *key, e->cached = true, v.push_back(e);
+    }
+  }
+  for (ShareSlot *c : stale) slot_free(c);
+  return e;
+}
+
+static void slot_release(ShareSlot *e, bool ok) {
+  if (e->cached) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    if (ok) {
+      e->busy = false;
+      return;
+    }
+    std::vector<ShareSlot *> &v = cache_slots();  // (a failed share's scene is not reused)
+    v.erase(std::remove(v.begin(), v.end(), e), v.end());
+  }
+  slot_free(e);
+}
+
+extern "C" void rt_render_cache_release(void) {
+  std::vector<ShareSlot *> idle;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    std::vector<ShareSlot *> &v = cache_slots();
+    for (ShareSlot *c : v) (c->busy ? (void)(c->cached = false) : idle.push_back(c));  // (a busy one: freed on release)
+    v.clear();
+  }
+  for (ShareSlot *c : idle) slot_free(c);
+}
+
 // ------------------------------------------------------------------------------ whole frame
 static std::mutex g_timing_mu;
 static std::vector<double> g_kernel_ms(64, 0.0);
+static std::vector<std::array<double, 4>> g_share_ms(64, std::array<double, 4>{0.0, 0.0, 0.0, 0.0});
 
 extern "C" double rt_last_kernel_ms(int device) {
   std::lock_guard<std::mutex> lk(g_timing_mu);
   return (device >= 0 && device < (int)g_kernel_ms.size()) ? g_kernel_ms[device] : 0.0;
 }
 
-// One device's share of rt_render: upload, launch, copy back its compact rows, scatter them into
-// rows j % G == g of the caller's buffer (disjoint rows: no lock).
-static int render_share(const rt_flat_scene *s, const HostPack &H, int g, int G, int device, uint8_t *out_host,
-                        std::string &err) {
+extern "C" int rt_last_share_ms(int share, double *ms) {
+  if (!ms) return rt_set_error("rt_last_share_ms: NULL argument"), -1;
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  if (share < 0 || share >= (int)g_share_ms.size()) return rt_set_error("rt_last_share_ms: share %d", share), -1;
+  for (int k = 0; k < 4; k++) ms[k] = g_share_ms[share][k];
+  return 0;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One share on one device: upload (or reuse), launch, copy its compact rows straight into rows
+// share + k * n_shares of the caller's buffer (disjoint rows: no lock), check completion.
+// pack() gives the host preprocessing (computed at most once per rt_render call, only on a miss).
+static int render_share(const rt_flat_scene *s, const std::function<const HostPack *()> &pack, const std::string *key,
+                        int g, int G, int device, uint8_t *out_host, std::string &err) {
+  const double t_start = now_ms();
   const int H_img = s->camera.height, W = s->camera.width;
   const int n_rows = (H_img - g + G - 1) / G;
-  rt_device_scene *scene = upload_packed(s, H, device);
-  if (!scene) {
-    err = rt_last_error();
-    return -1;
-  }
-  hipStream_t stream = nullptr;
-  uint8_t *d_out = nullptr;
-  hipEvent_t t0 = nullptr, t1 = nullptr;
+  ShareSlot *e = slot_acquire(key, device, g, G);
   int rc = 0;
-  std::vector<uint8_t> rows((size_t)n_rows * W * 3);
-  if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&d_out, rows.size()) != hipSuccess || hipEventCreate(&t0) != hipSuccess ||
-      hipEventCreate(&t1) != hipSuccess) {
-    rt_set_error("rt_render: stream/buffer setup failed on device %d", g);
+  if (!e->scene) {
+    const HostPack *H = pack();
+    e->scene = H ? upload_packed(s, *H, device) : nullptr;
+    if (!e->scene ||
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&e->d_out, (size_t)n_rows * W * 3) != hipSuccess) {
+      if (e->scene) rt_set_error("rt_render: stream/buffer setup failed on device %d", device);
+      rc = -1;
+    }
+  }
+  const double t_setup = now_ms();
+  double t_done = t_setup;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (rc == 0 && (hipSetDevice(device) != hipSuccess || hipEventCreate(&t0) != hipSuccess ||
+                  hipEventCreate(&t1) != hipSuccess)) {
+    rt_set_error("rt_render: event setup failed on device %d", device);
     rc = -1;
   }
   if (rc == 0) {
-    (void)hipEventRecord(t0, stream);
-    rc = rt_render_rows_async(scene, g, G, n_rows, d_out, stream);
-    (void)hipEventRecord(t1, stream);
+    (void)hipEventRecord(t0, e->stream);
+    rc = rt_render_rows_async(e->scene, g, G, n_rows, e->d_out, e->stream);
+    (void)hipEventRecord(t1, e->stream);
   }
   if (rc == 0) {
-    hipError_t e = hipStreamSynchronize(stream);
-    if (e == hipSuccess) e = hipMemcpy(rows.data(), d_out, rows.size(), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-      rt_set_error("rt_render: share %d (device %d): %s", g, device, hipGetErrorString(e));
+    hipError_t x = hipEventSynchronize(t1);
+    t_done = now_ms();
+    const size_t row = (size_t)W * 3;
+    if (x == hipSuccess)
+      x = hipMemcpy2DAsync(out_host + (size_t)g * row, row * (size_t)G, e->d_out, row, row, (size_t)n_rows,
+                           hipMemcpyDeviceToHost, e->stream);
+    if (x == hipSuccess) x = hipStreamSynchronize(e->stream);
+    if (x != hipSuccess) {
+      rt_set_error("rt_render: share %d (device %d): %s", g, device, hipGetErrorString(x));
       rc = -1;
-    } else if (rt_scene_check(scene) != 0) {  // never a partial image with rc 0
+    } else if (rt_scene_check(e->scene) != 0) {  // never a partial image with rc 0
       rc = -1;
-    } else {
-      float ms = 0.0f;
-      (void)hipEventElapsedTime(&ms, t0, t1);
-      {
-        std::lock_guard<std::mutex> lk(g_timing_mu);
-        if (g < (int)g_kernel_ms.size()) g_kernel_ms[g] = ms;
-      }
-      for (int k = 0; k < n_rows; k++)
-        memcpy(out_host + (size_t)(g + k * G) * W * 3, rows.data() + (size_t)k * W * 3, (size_t)W * 3);
+    }
+  }
+  if (rc == 0) {
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, t0, t1);
+    const double t_end = now_ms();
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    if (g < (int)g_kernel_ms.size()) {
+      g_kernel_ms[g] = ms;
+      g_share_ms[g] = {t_setup - t_start, t_done - t_setup, t_end - t_done, t_end - t_start};
     }
   }
   if (rc != 0) err = rt_last_error();
   (void)hipSetDevice(device);
   if (t0) (void)hipEventDestroy(t0);
   if (t1) (void)hipEventDestroy(t1);
-  if (d_out) (void)hipFree(d_out);
-  if (stream) (void)hipStreamDestroy(stream);
-  rt_scene_release(scene);
+  slot_release(e, rc == 0);
   return rc;
 }
 
@@ -2004,23 +2163,59 @@ extern "C" int rt_render(const rt_flat_scene *s, int n_gpus, uint8_t *out_host) 
   const int visible = rehearse > 0 ? rehearse : avail;
   int G = (n_gpus <= 0 || n_gpus > visible) ? visible : n_gpus;
   if (G > s->camera.height) G = s->camera.height;
-  HostPack H;  // host preprocessing once, shared by every device
-  if (host_pack(s, H) != 0) return -1;
   const int per_dev = (G + avail - 1) / avail;  // shares per device (> 1 only when rehearsing)
-  if (per_dev > 1) H.cfg.chain_mb /= (size_t)per_dev;
+  std::string key;
+  const bool cache = env_int("RT_SCENE_CACHE", 1) != 0;
+  if (cache) key = scene_key(s, per_dev);
+  // host preprocessing at most once, shared by every device, and only when a share has no cached scene
+  HostPack H;
+  int pack_rc = 0;
+  std::once_flag once;
+  auto pack = [&]() -> const HostPack * {
+    std::call_once(once, [&] {
+      pack_rc = host_pack(s, H);
+      if (per_dev > 1) H.cfg.chain_mb /= (size_t)per_dev;
+    });
+    return pack_rc == 0 ? &H : nullptr;
+  };
   std::vector<int> rc(G, 0);
   std::vector<std::string> err(G);
   if (G == 1) {
-    rc[0] = render_share(s, H, 0, 1, 0, out_host, err[0]);
+    rc[0] = render_share(s, pack, cache ? &key : nullptr, 0, 1, 0, out_host, err[0]);
   } else {  // one host thread per share: uploads and launches proceed in parallel
     std::vector<std::thread> th;
     for (int g = 0; g < G; g++)
-      th.emplace_back([&, g] { rc[g] = render_share(s, H, g, G, g % avail, out_host, err[g]); });
+      th.emplace_back([&, g] { rc[g] = render_share(s, pack, cache ? &key : nullptr, g, G, g % avail, out_host, err[g]); });
     for (auto &t : th) t.join();
   }
   for (int g = 0; g < G; g++)
     if (rc[g] != 0) return rt_set_error("%s", err[g].c_str()), -1;
   return 0;
+}
+
+// One share of rt_render's partition, for a driver that runs one process (or thread) per GPU: rows
+// j % n_shares == share of the frame on `device`, written into those rows of out_host (a whole frame's
+// buffer; the other rows are left as they are).  Same cache and completion check as rt_render.
+extern "C" int rt_render_share(const rt_flat_scene *s, int share, int n_shares, int device, uint8_t *out_host) {
+  if (!s || !out_host) return rt_set_error("rt_render_share: NULL argument"), -1;
+  if (n_shares < 1 || share < 0 || share >= n_shares || share >= s->camera.height)
+    return rt_set_error("rt_render_share: share %d of %d (image height %d)", share, n_shares, s->camera.height), -1;
+  const int avail = rt_device_count();
+  if (avail <= 0) return rt_set_error("rt_render_share: no HIP device visible (this library has no CPU path)"), -1;
+  if (device < 0 || device >= avail) return rt_set_error("rt_render_share: device %d of %d", device, avail), -1;
+  std::string key;
+  const bool cache = env_int("RT_SCENE_CACHE", 1) != 0;
+  if (cache) key = scene_key(s, 1);
+  HostPack H;
+  int pack_rc = 1;
+  auto pack = [&]() -> const HostPack * {
+    if (pack_rc == 1) pack_rc = host_pack(s, H);
+    return pack_rc == 0 ? &H : nullptr;
+  };
+  std::string err;
+  const int rc = render_share(s, pack, cache ? &key : nullptr, share, n_shares, device, out_host, err);
+  if (rc != 0) rt_set_error("%s", err.c_str());
+  return rc;
 }
 
 extern "C" int rt_diag_libm(int fn, const float *x_host, float *out_host, int64_t n, int device) {

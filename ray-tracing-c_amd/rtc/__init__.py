@@ -157,6 +157,13 @@ def lib() -> ctypes.CDLL:
         L.rt_render.restype = c_int
         L.rt_last_kernel_ms.argtypes = [c_int]
         L.rt_last_kernel_ms.restype = c_double
+        if hasattr(L, "rt_render_share"):  # (older builds loaded through RTC_LIB for an A/B lack these)
+            L.rt_render_share.argtypes = [P, c_int, c_int, c_int, c_void_p]
+            L.rt_render_share.restype = c_int
+            L.rt_render_cache_release.argtypes = []
+            L.rt_render_cache_release.restype = None
+            L.rt_last_share_ms.argtypes = [c_int, c_void_p]
+            L.rt_last_share_ms.restype = c_int
         L.rt_diag_libm.argtypes = [c_int, c_void_p, c_void_p, c_int64, c_int]
         L.rt_diag_libm.restype = c_int
         L.rt_diag_arith.argtypes = [c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_int]
@@ -271,6 +278,34 @@ def render(scene: Scene, n_gpus: int = 1) -> np.ndarray:
     if rc != 0:
         raise RtcError(f"rt_render failed: {last_error(L)}")
     return out
+
+
+def render_share(scene: Scene, share: int, n_shares: int, device: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    """Rows j % n_shares == share of the frame on `device` (rt_render_share: what one process per GPU
+    runs), written into those rows of `out` (a whole (H, W, 3) uint8 frame; a new zeroed one if None)."""
+    if out is None:
+        out = np.zeros((scene.height, scene.width, 3), dtype=np.uint8)
+    if out.shape != (scene.height, scene.width, 3) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous (H, W, 3) uint8 array")
+    L = lib()
+    rc = L.rt_render_share(scene.ptr, int(share), int(n_shares), int(device), out.ctypes.data)
+    if rc != 0:
+        raise RtcError(f"rt_render_share failed: {last_error(L)}")
+    return out
+
+
+def release_cache() -> None:
+    """Free the device scenes rt_render / rt_render_share keep between calls (rt_render_cache_release)."""
+    lib().rt_render_cache_release()
+
+
+def last_share_ms(share: int = 0) -> dict:
+    """Host wall-clock phases of the last call's share `share` (rt_last_share_ms): setup (upload and
+    allocations), run (launch to finish), d2h (rows back, completion check), total -- in ms."""
+    buf = (c_double * 4)()
+    if lib().rt_last_share_ms(int(share), buf) != 0:
+        raise RtcError(f"rt_last_share_ms: {last_error()}")
+    return dict(zip(("setup", "run", "d2h", "total"), (float(x) for x in buf)))
 
 
 def last_kernel_ms(device: int = 0) -> float:

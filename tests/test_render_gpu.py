@@ -275,9 +275,11 @@ def test_chain_render_north_star_scene(manifest, env, monkeypatch):
 
 def test_chain_record_arena_clean_across_launches(manifest, monkeypatch):
     """The record arena is clean between chain launches only because each launch's cost pre-pass sets
-    the previous launch's reservation back (rt_book1.h: clean_records; no fill after the plan): launches
-    of shrinking and growing reservations on one device scene -- the whole frame, eight and two rank
-    shares, the whole frame again -- must each reproduce the reference rows."""
+    the previous launch's reservation back (rt_book1.h: clean_records) and a fresh arena's records are
+    filled only as far as a launch reserves past the clean high-water mark (chain_fill_kernel, r06):
+    launches of growing and shrinking reservations on one device scene -- two rank shares of a fresh
+    arena, the whole frame (growing past them), eight and two rank shares, the whole frame again -- must
+    each reproduce the reference rows."""
     import torch
 
     monkeypatch.setenv("RT_MODE", "chain")
@@ -290,7 +292,7 @@ def test_chain_record_arena_clean_across_launches(manifest, monkeypatch):
         sc = rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"])
         ds = rtc.DeviceScene(sc, 0)
     stream = torch.cuda.current_stream(0)
-    for world, ranks in ((1, [0]), (8, range(8)), (2, range(2)), (1, [0]), (8, [7, 0])):
+    for world, ranks in ((8, [7, 0]), (1, [0]), (8, range(8)), (2, range(2)), (1, [0]), (8, [7, 0])):
         for rank in ranks:
             row0, stride, n = rtc.rows_of(sc.height, rank, world)
             buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda:0")
@@ -429,3 +431,44 @@ def test_dropin_reference_main_on_eight_rehearsed_devices(manifest, tmp_path):
     data = open(os.path.join(str(tmp_path), "output.tiff"), "rb").read()
     e = manifest["renders"]["s1_1200x675_10spp_d50"]
     assert hashlib.sha256(data[168:]).hexdigest() == e["sha256"]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_render_share_reassembles_reference_frame(manifest, world, monkeypatch):
+    """rt_render_share (one process or thread per GPU, r06): every share of a `world`-way partition,
+    written into one host frame, is the reference frame -- from an empty device-scene cache, again from
+    the warm cache (no upload: the scene, its record arena and its rows reused), and with the cache off."""
+    e = manifest["renders"]["s1_1200x675_10spp_d50"]
+    sc = rtc.Scene.preset(1, 1200, 10, 50)
+    for cache in ("1", "1", "0"):
+        monkeypatch.setenv("RT_SCENE_CACHE", cache)
+        out = np.zeros((sc.height, sc.width, 3), np.uint8)
+        for g in range(world):
+            rtc.render_share(sc, g, world, 0, out)
+            ms = rtc.last_share_ms(g)
+            assert ms["total"] >= ms["run"] > 0.0
+        assert hashlib.sha256(out.tobytes()).hexdigest() == e["sha256"], (world, cache)
+    with pytest.raises(rtc.RtcError, match="share"):
+        rtc.render_share(sc, world, world, 0)
+    rtc.release_cache()
+
+
+def test_device_scene_cache_follows_scene_and_environment(manifest, monkeypatch):
+    """The device-scene cache is keyed by the flat scene's bytes and the RT_* environment: alternating
+    scenes, spp and a planner knob between rt_render calls must give each configuration's reference
+    frame, never a frame of the previously cached scene; rt_render_cache_release empties it."""
+    names = ["s1_300x168_16spp_d50", "s0_400x225_100spp_d50", "s1_300x168_16spp_d50", "s5_200x112_16spp_d50",
+             "s1_300x168_16spp_d50"]
+    for i, name in enumerate(names):
+        e = manifest["renders"][name]
+        if i == 2:
+            monkeypatch.setenv("RT_CHAIN_BETA", "0.5")  # (another key: a new plan, the same frame)
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))
+        _check(img, golden_image(e), f"{name} (call {i})")
+        img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]))  # warm
+        _check(img, golden_image(e), f"{name} (call {i}, warm)")
+        assert rtc.last_share_ms(0)["setup"] < 1000.0
+    rtc.release_cache()
+    e = manifest["renders"]["s1_300x168_16spp_d50"]
+    img = rtc.render(rtc.Scene.preset(e["scene"], e["width"], e["spp"], e["depth"]), n_gpus=1)
+    _check(img, golden_image(e), "after rt_render_cache_release")
