@@ -109,7 +109,10 @@ int rt_diag_arith(int fn, uint64_t start, uint64_t count, uint64_t seed, unsigne
 
 /* Milliseconds of the last frame launch rt_render_rows_async made for `dscene` (HIP events on its
  * stream; call after that work completed).  Excludes the cost pre-pass and the plan
- * (rt_book1_cost_kernel, chain_* planner kernels).  -1 when unavailable. */
+ * (rt_book1_cost_kernel, chain_* planner kernels).  -1 when unavailable.  Since r05 the pre-pass renders
+ * each pixel's first samples (up to 64) and the frame launch goes on from them, so this excludes part of
+ * the frame's sample work: compare whole steps (pre-pass + plan + frame launch + fold) across builds,
+ * not this number (bench.py's roofline uses the step time). */
 double rt_scene_last_launch_ms(rt_device_scene *dscene);
 
 /* The same for the scene's last min(max, 64) launches, oldest first, into ms[]: returns how many were
@@ -123,7 +126,8 @@ int rt_scene_launch_history(rt_device_scene *dscene, double *ms, int max);
  * bit 1 ended), link segment, link record, segment length (draws), the pixel's pre-pass draws, the
  * pixel's own pre-pass cost (traversal steps), the tick at which a helper wave took the item over (tail
  * migration; 0: never migrated), the planner's cost of the pixel (max(own, row-neighbour mean) when
- * cost smoothing is on, else the own cost), 1 reserved (0).
+ * cost smoothing is on, else the own cost), where the item started (XCC_ID << 28 | HW_ID bits 0-15: wave,
+ * SIMD, pipe, CU, SH, SE; 0 for items a helper started).
  * Returns the number of items (at most max_rows rows are written), -1 on error. */
 int64_t rt_scene_chain_diag(rt_device_scene *dscene, uint32_t *rows, int64_t max_rows);
 

@@ -877,11 +877,23 @@ RT_D bool chain_walk_done(const Book1View &V, const ChainPx &P, uint32_t k, uint
 RT_D bool chain_boundary_(const Book1View &V, int64_t pix, uint32_t seg, uint32_t x, uint32_t s, f3 acc,
                           uint32_t &tc, uint32_t &st, uint8_t *__restrict__ out, bool writer);
 // (diagnostic timeline, RT_PX_TIME=1: a chain's start and end in wall_clock64 ticks)
+// (word 3: where the item started -- XCC_ID << 28 | HW_ID's wave, SIMD, pipe, CU, SH and SE fields)
+constexpr int kTimeWords = 4;
+RT_D uint32_t hw_where() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));      // HW_REG_HW_ID, 32 bits
+  const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));     // HW_REG_XCC_ID, 4 bits
+  return (xcc << 28) | (hw & 0xffffu);
+#else
+  return 0u;
+#endif
+}
 RT_D void chain_time(const Book1View &V, int64_t pix, uint32_t seg, int end) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t now = (uint32_t)wall_clock64();
-  if (seg & kItemUnsplit) V.px_time[3 * pix + end] = now;
-  else V.seg_time[3 * (V.ch_px[pix].end0 + seg) + end] = now;
+  uint32_t *w = (seg & kItemUnsplit) ? V.px_time + kTimeWords * pix : V.seg_time + kTimeWords * (V.ch_px[pix].end0 + seg);
+  w[end] = now;
+  if (end == 0) w[3] = hw_where();
 #endif
 }
 RT_D bool chain_boundary(const Book1View &V, int64_t pix, uint32_t seg, uint32_t x, uint32_t s, f3 acc,
@@ -1094,8 +1106,8 @@ RT_D void render_item_coop(const Book1View &V, const float4 *items9, int64_t pix
 #endif
   if (kMode != 2 && lane0) write_pixel(out + pix * 3, acc, cam.spp);
   if (V.px_time && lane0 && kMode != 2) {
-    if (!res) V.px_time[3 * pix] = px_start;
-    V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
+    if (!res) V.px_time[kTimeWords * pix] = px_start;
+    V.px_time[kTimeWords * pix + 1] = (uint32_t)wall_clock64();
   }
 }
 
@@ -1459,7 +1471,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
             V.draw_out[pix] = cut ? (uint32_t)((uint64_t)g.n * spp / s) : g.n;
             if (V.pre_state) V.pre_state[pix] = make_float4(acc.x, acc.y, acc.z, u2f(pre_word(g.n, (uint32_t)s)));
           }
-          if (V.px_time) V.px_time[3 * pix + 1] = (uint32_t)wall_clock64();
+          if (V.px_time) V.px_time[kTimeWords * pix + 1] = (uint32_t)wall_clock64();
           if (kMode == kMigMode && V.mig_live > 0) mig_item_done(V, total_own);
           need_pixel = true;
         } else {
@@ -1510,7 +1522,7 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
         }
         need_pixel = false;
         px_steps = 0;
-        if (V.px_time && kMode != 2) V.px_time[3 * pix] = (uint32_t)wall_clock64();
+        if (V.px_time && kMode != 2) V.px_time[kTimeWords * pix] = (uint32_t)wall_clock64();
         if (V.px_time && kMode == 2 && !cont) chain_time(V, pix, seg, 0);
       }
       if (kMode == 2 && chain_boundary(V, pix, seg, g.n, (uint32_t)s, acc, tc, st, out, true)) {

@@ -98,6 +98,9 @@ RT_D bool runs_push(PathRuns &R, uint32_t code) {
 #ifndef RT_GEN_XREG
 #define RT_GEN_XREG 1  // explicit albedos in registers
 #endif
+#ifndef RT_GEN_SLOT_MAJOR
+#define RT_GEN_SLOT_MAJOR 0
+#endif
 constexpr int kWReg = RT_GEN_WREG, kXReg = RT_GEN_XREG;
 template <int kN>
 struct RegStack {
@@ -105,11 +108,11 @@ struct RegStack {
   int n;  // entries pushed and not popped (the newest min(n, kN) in v, newest first)
 };
 template <int kN>
-RT_D void rs_push(RegStack<kN> &S, float x, float *spill) {
+RT_D void rs_push(RegStack<kN> &S, float x, float *spill, uint32_t stride = 1) {
   if constexpr (kN == 0) {
-    spill[S.n] = x;
+    spill[(uint32_t)S.n * stride] = x;
   } else {
-    if (S.n >= kN) spill[S.n - kN] = S.v[kN - 1];
+    if (S.n >= kN) spill[(uint32_t)(S.n - kN) * stride] = S.v[kN - 1];
 #pragma unroll
     for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
     S.v[0] = x;
@@ -117,15 +120,15 @@ RT_D void rs_push(RegStack<kN> &S, float x, float *spill) {
   S.n++;
 }
 template <int kN>
-RT_D float rs_pop(RegStack<kN> &S, const float *spill) {
+RT_D float rs_pop(RegStack<kN> &S, const float *spill, uint32_t stride = 1) {
   S.n--;
   if constexpr (kN == 0) {
-    return spill[S.n];
+    return spill[(uint32_t)S.n * stride];
   } else {
     const float x = S.v[0];
 #pragma unroll
     for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
-    if (S.n >= kN) S.v[kN - 1] = spill[S.n - kN];
+    if (S.n >= kN) S.v[kN - 1] = spill[(uint32_t)(S.n - kN) * stride];
     return x;
   }
 }
@@ -135,11 +138,11 @@ struct XStack {  // explicit albedos
   int n;
 };
 template <int kN>
-RT_D void xs_push(XStack<kN> &S, f3 x, float4 *spill) {
+RT_D void xs_push(XStack<kN> &S, f3 x, float4 *spill, uint32_t stride = 1) {
   if constexpr (kN == 0) {
-    spill[S.n] = make_float4(x.x, x.y, x.z, 0.0f);
+    spill[(uint32_t)S.n * stride] = make_float4(x.x, x.y, x.z, 0.0f);
   } else {
-    if (S.n >= kN) spill[S.n - kN] = make_float4(S.v[kN - 1].x, S.v[kN - 1].y, S.v[kN - 1].z, 0.0f);
+    if (S.n >= kN) spill[(uint32_t)(S.n - kN) * stride] = make_float4(S.v[kN - 1].x, S.v[kN - 1].y, S.v[kN - 1].z, 0.0f);
 #pragma unroll
     for (int k = kN - 1; k > 0; k--) S.v[k] = S.v[k - 1];
     S.v[0] = x;
@@ -147,17 +150,17 @@ RT_D void xs_push(XStack<kN> &S, f3 x, float4 *spill) {
   S.n++;
 }
 template <int kN>
-RT_D f3 xs_pop(XStack<kN> &S, const float4 *spill) {
+RT_D f3 xs_pop(XStack<kN> &S, const float4 *spill, uint32_t stride = 1) {
   S.n--;
   if constexpr (kN == 0) {
-    const float4 e = spill[S.n];
+    const float4 e = spill[(uint32_t)S.n * stride];
     return mk(e.x, e.y, e.z);
   } else {
     const f3 x = S.v[0];
 #pragma unroll
     for (int k = 0; k < kN - 1; k++) S.v[k] = S.v[k + 1];
     if (S.n >= kN) {
-      const float4 e = spill[S.n - kN];
+      const float4 e = spill[(uint32_t)(S.n - kN) * stride];
       S.v[kN - 1] = mk(e.x, e.y, e.z);
     }
     return x;
@@ -205,12 +208,13 @@ RT_D void rec_clear(PathRecord<kW, kX> &P) {  // a new sample
 // plus the weighted bit when it has a pdf weight w (else w is 1.0f and unused).  xrec / xw: the thread's
 // kMaxDepth slots for what leaves the register stacks.
 template <int kW, int kX>
-RT_D void rec_push(PathRecord<kW, kX> &P, uint32_t code, f3 albedo, float w, float4 *xrec, float *xw) {
+RT_D void rec_push(PathRecord<kW, kX> &P, uint32_t code, f3 albedo, float w, float4 *xrec, float *xw,
+                   uint32_t stride = 1) {
   const uint32_t code_explicit = (1u << P.runs.cb) - 1u, code_weighted = 1u << P.runs.cb;
   if (!runs_push(P.runs, code)) code = code_explicit | code_weighted;  // past the runs: explicit, weighted
-  if ((code & code_explicit) == code_explicit) xs_push(P.xst, albedo, xrec);
+  if ((code & code_explicit) == code_explicit) xs_push(P.xst, albedo, xrec, stride);
   if ((code & code_weighted) && w == 2.0f) P.w2 |= 1ull << P.n;
-  else if (code & code_weighted) rs_push(P.wst, w, xw);
+  else if (code & code_weighted) rs_push(P.wst, w, xw, stride);
   P.nonfin |= (uint32_t)!__builtin_isfinite(albedo.x) | ((uint32_t)!__builtin_isfinite(albedo.y) << 1) |
               ((uint32_t)!__builtin_isfinite(albedo.z) << 2) | (__builtin_isfinite(w) ? 0u : 7u);
   P.n++;
@@ -223,7 +227,8 @@ RT_D void rec_push(PathRecord<kW, kX> &P, uint32_t code, f3 albedo, float w, flo
 // reloading the records stored beyond the registers (scene 7: 48 % of paths, holding 54 % of those
 // entries).  acc + (+0) == acc bit for bit (acc is never -0: it starts at +0).
 template <int kW, int kX, typename Colors>
-RT_D f3 rec_fold(PathRecord<kW, kX> &P, f3 tail, const Colors &colors, const float4 *xrec, const float *xw) {
+RT_D f3 rec_fold(PathRecord<kW, kX> &P, f3 tail, const Colors &colors, const float4 *xrec, const float *xw,
+                 uint32_t stride = 1) {
   if (tail.x == 0.0f && tail.y == 0.0f && tail.z == 0.0f && P.nonfin == 0u) return mk(0.0f, 0.0f, 0.0f);
   const PathRuns &R = P.runs;
   const uint32_t code_explicit = (1u << R.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << R.cb;
@@ -246,9 +251,9 @@ RT_D f3 rec_fold(PathRecord<kW, kX> &P, f3 tail, const Colors &colors, const flo
       }
       left--;
     }
-    if ((code & code_explicit) == code_explicit) a = xs_pop(P.xst, xrec);
+    if ((code & code_explicit) == code_explicit) a = xs_pop(P.xst, xrec, stride);
     f3 x = mul(a, c);
-    if (code & code_weighted) x = scale(x, (P.w2 >> k) & 1ull ? 2.0f : rs_pop(P.wst, xw));
+    if (code & code_weighted) x = scale(x, (P.w2 >> k) & 1ull ? 2.0f : rs_pop(P.wst, xw, stride));
     c = add(mk(0.0f, 0.0f, 0.0f), x);
   }
   return c;
@@ -288,10 +293,29 @@ RT_D void pre_frame_terms(PreTrace &T) {
   T.ra = recip_core(T.dd);
   T.fast = T.dd >= kDivLo && T.dd <= kDivHi;
 }
+// A preorder array: entries as (q0, q1) pairs -- the global S.pre -- or, under RT_GEN_SPLIT, the LDS copy
+// as two arrays, every entry's q0 then every entry's q1 `half` entries further (rt_book1.h's item split:
+// a ds_read_b128 of random entries then spreads over every bank instead of half of them).
+struct PrePairs {
+  const float4 *p;
+  RT_D float4 q0(uint32_t q) const { return p[2 * q]; }
+  RT_D float4 q1(uint32_t q) const { return p[2 * q + 1]; }
+};
+struct PreSplit {
+  const float4 *p;
+  uint32_t half;
+  RT_D float4 q0(uint32_t q) const { return p[q]; }
+  RT_D float4 q1(uint32_t q) const { return p[half + q]; }
+};
+#ifndef RT_GEN_SPLIT
+#define RT_GEN_SPLIT 0
+#endif
+
 // Apply the transform of preorder entry `pos` to (o, d): one step of local_ray's chain (translate:
 // o - offset; rotate_y: rot_y of o and d), from the entry's inline words.
-RT_D void pre_apply_xform(const float4 *pre, uint32_t pos, f3 &o, f3 &d) {
-  const float4 q0 = pre[2 * pos], q1 = pre[2 * pos + 1];
+template <typename PA>
+RT_D void pre_apply_xform(PA pre, uint32_t pos, f3 &o, f3 &d) {
+  const float4 q0 = pre.q0(pos), q1 = pre.q1(pos);
   if (rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, q1.w)) == RT_KIND_TRANSLATE) {
     o = sub(o, mk(q0.y, q0.w, q1.x));
   } else {
@@ -301,13 +325,14 @@ RT_D void pre_apply_xform(const float4 *pre, uint32_t pos, f3 &o, f3 &d) {
 }
 // The ray in the frame whose transform entry is at `pos` (~0: the world), from the world ray:
 // local_ray's chain outermost first, walking the entries' enclosing positions (depth <= 8).
-RT_D void pre_chain_ray(const float4 *pre, uint32_t pos, f3 wo, f3 wd, f3 &o, f3 &d) {
+template <typename PA>
+RT_D void pre_chain_ray(PA pre, uint32_t pos, f3 wo, f3 wd, f3 &o, f3 &d) {
   int depth = 0;
-  for (uint32_t q = pos; q != 0xffffffffu && depth < 8; q = __builtin_bit_cast(uint32_t, pre[2 * q].z)) depth++;
+  for (uint32_t q = pos; q != 0xffffffffu && depth < 8; q = __builtin_bit_cast(uint32_t, pre.q0(q).z)) depth++;
   o = wo, d = wd;
   for (int lvl = depth - 1; lvl >= 0; lvl--) {
     uint32_t q = pos;
-    for (int k = 0; k < lvl; k++) q = __builtin_bit_cast(uint32_t, pre[2 * q].z);
+    for (int k = 0; k < lvl; k++) q = __builtin_bit_cast(uint32_t, pre.q0(q).z);
     pre_apply_xform(pre, q, o, d);
   }
 }
@@ -344,18 +369,18 @@ RT_D bool pre_is_rare(const PreTrace &T, float4 q1) {
 // One action of the scan (pre_step's, for the entry q0/q1 at T.p); true once past the last entry.
 // Leaving transform subtrees is an action of its own: the entry at T.p then runs in a later step.
 // pre: the preorder (S.pre, or its LDS copy when the whole of it is there: plain ds_read, no flat).
-template <int F>
-RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g, float4 q0,
+template <int F, typename PA>
+RT_D bool pre_exec(const DScene &S, PA pre, PreTrace &T, f3 wo, f3 wd, float tmin, Pcg32 &g, float4 q0,
                    float4 q1) {
   const uint32_t n = (uint32_t)S.n_pre;
   if (T.p >= n) return true;
   if ((F & RT_FEAT_XFORM) && T.p >= T.fend) {
     uint32_t pp;
     do {  // leaving a transform's subtree: the enclosing frame again (its ref sits in its entry)
-      pp = __builtin_bit_cast(uint32_t, pre[2 * T.fpos].z);
+      pp = __builtin_bit_cast(uint32_t, pre.q0(T.fpos).z);
       const bool top = pp == 0xffffffffu;
-      T.frame = top ? RT_REF_NONE : (int32_t)__builtin_bit_cast(uint32_t, pre[2 * pp + 1].w);
-      T.fend = top ? 0xffffffffu : __builtin_bit_cast(uint32_t, pre[2 * pp].x);
+      T.frame = top ? RT_REF_NONE : (int32_t)__builtin_bit_cast(uint32_t, pre.q1(pp).w);
+      T.fend = top ? 0xffffffffu : __builtin_bit_cast(uint32_t, pre.q0(pp).x);
       T.fpos = top ? 0u : pp;
     } while (T.p >= T.fend);
     pre_chain_ray(pre, pp, wo, wd, T.o, T.d);
@@ -486,8 +511,8 @@ RT_D bool pre_exec(const DScene &S, const float4 *pre, PreTrace &T, f3 wo, f3 wd
 // Results equal pre_exec's for the same entry.  Precondition: T.p < n (a tracing lane's entry).
 // (Sphere / quad lanes waiting for company while lanes sit at boxes, as rt_book1.h's measured leaf
 // wait: 8 / 16 lanes 14 / 58 % slower on config 5, r04.)
-template <int F>
-RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin, float4 q0, float4 q1,
+template <int F, typename PA>
+RT_D bool pre_common(const DScene &S, PA pre, PreTrace &T, float tmin, float4 q0, float4 q1,
                      int extra = 0) {
   const int32_t ref = (int32_t)__builtin_bit_cast(uint32_t, q1.w);
   const int kind = rt_ref_kind(ref);
@@ -557,7 +582,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   for (int e = 0; e < 2; e++) {
     const bool go = more && extra > e && next < (uint32_t)S.n_pre && next < T.fend;
     const uint32_t q = go ? next : T.p;
-    const float4 r0 = pre[2 * q], r1 = pre[2 * q + 1];
+    const float4 r0 = pre.q0(q), r1 = pre.q1(q);
     const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
     const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
     const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
@@ -569,7 +594,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
 #else
   bool more = extra > 0 && next < (uint32_t)S.n_pre && next < T.fend;
   if (more) {
-    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float4 r0 = pre.q0(next), r1 = pre.q1(next);
     const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
     const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
     const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
@@ -580,7 +605,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
   }
   // the second extra action straight-line as well (extra == 2, the default), further ones looped
   if (more && extra >= 2 && next < (uint32_t)S.n_pre && next < T.fend) {
-    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float4 r0 = pre.q0(next), r1 = pre.q1(next);
     const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
     const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
     const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
@@ -592,7 +617,7 @@ RT_D bool pre_common(const DScene &S, const float4 *pre, PreTrace &T, float tmin
 #endif
 #pragma unroll 1
   for (int e = 2; more && e < extra && next < (uint32_t)S.n_pre && next < T.fend; e++) {
-    const float4 r0 = pre[2 * next], r1 = pre[2 * next + 1];
+    const float4 r0 = pre.q0(next), r1 = pre.q1(next);
     const float cx = (r0.x - o.x) * ix, dx = (r0.w - o.x) * ix;
     const float cy = (r0.y - o.y) * iy, dy = (r1.x - o.y) * iy;
     const float cz = (r0.z - o.z) * iz, dz = (r1.y - o.z) * iz;
@@ -626,7 +651,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
     pl.grad = pg;
   }
   if (n_lds) {  // the top of the preorder (the first BVH levels of every root item) in LDS
+#if RT_GEN_SPLIT
+    for (uint32_t q = threadIdx.x; q < n_lds; q += blockDim.x) lds[q] = S.pre[2 * q], lds[n_lds + q] = S.pre[2 * q + 1];
+#else
     for (uint32_t q = threadIdx.x; q < 2 * n_lds; q += blockDim.x) lds[q] = S.pre[q];
+#endif
   }
   if (n_lds || pl.perm) __syncthreads();
   constexpr bool kFull = (F & (RT_FEAT_EMISSIVE | RT_FEAT_LIGHTS)) != 0;
@@ -649,7 +678,13 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
   PathRecord<kWReg, kXReg> P;
   rec_init(P, V.code_bits);
   const uint32_t code_explicit = (1u << P.runs.cb) - 1u, code_unit = code_explicit - 1u, code_weighted = 1u << P.runs.cb;
-  const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth;
+#if RT_GEN_SLOT_MAJOR
+  // slot-major: entry k of every thread's slots is one array, so a wave's pushes at equal depth are
+  // neighbouring words (thread-contiguous slots put them kMaxDepth entries apart, one line each)
+  const uint32_t rec0 = blockIdx.x * blockDim.x + threadIdx.x, rec_stride = gridDim.x * blockDim.x;
+#else
+  const uint32_t rec0 = (blockIdx.x * blockDim.x + threadIdx.x) * (uint32_t)kMaxDepth, rec_stride = 1u;
+#endif
   const auto solid_color = [&](uint32_t t) { return ld3(S.textures[t].color); };
   // extra box actions per step: RT_GEN_FLAT - 1 in the diagnostic build; the product's 2 at compile time,
   // so pre_common's loop for further ones -- and its per-step exec-mask bookkeeping -- compiles away
@@ -751,7 +786,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           int kind = -1;
           if (on) {
             const uint32_t q = T.p;
-            const float4 q1 = q < n_lds ? lds[2 * q + 1] : S.pre[2 * q + 1];
+            const float4 q1 = q < n_lds ? lds[RT_GEN_SPLIT ? n_lds + q : 2 * q + 1] : S.pre[2 * q + 1];
             kind = rt_ref_kind((int32_t)__builtin_bit_cast(uint32_t, q1.w));
           }
           const uint64_t b0 = __ballot(on && kind == RT_KIND_BVH), b1 = __ballot(on && kind == RT_KIND_SPHERE),
@@ -780,7 +815,11 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             typedef float f4v __attribute__((ext_vector_type(4)));
             f4v v0, v1;
             if (kAllLds || q < n_lds) {
+#if RT_GEN_SPLIT
+              v0 = *(const f4v *)&lds[q], v1 = *(const f4v *)&lds[n_lds + q];
+#else
               v0 = *(const f4v *)&lds[2 * q], v1 = *(const f4v *)&lds[2 * q + 1];
+#endif
             } else {
               v0 = *(const f4v *)&S.pre[2 * q], v1 = *(const f4v *)&S.pre[2 * q + 1];
             }
@@ -793,10 +832,16 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
             bool fin = false;
             GS_ADD(kGsCycClassify, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && !rare) fin = pre_common<F>(S, kAllLds ? lds : S.pre, T, 1e-3f, q0, q1, extra_boxes);
+            if (tracing && !rare) {
+              if constexpr (kAllLds && RT_GEN_SPLIT) fin = pre_common<F>(S, PreSplit{lds, n_lds}, T, 1e-3f, q0, q1, extra_boxes);
+              else fin = pre_common<F>(S, PrePairs{kAllLds ? lds : S.pre}, T, 1e-3f, q0, q1, extra_boxes);
+            }
             GS_ADD(kGsCycCommon, GS_NOW() - gs_c);
             gs_c = GS_NOW();
-            if (tracing && rare && run_rare) fin = pre_exec<F>(S, kAllLds ? lds : S.pre, T, o, d, 1e-3f, g, q0, q1);
+            if (tracing && rare && run_rare) {
+              if constexpr (kAllLds && RT_GEN_SPLIT) fin = pre_exec<F>(S, PreSplit{lds, n_lds}, T, o, d, 1e-3f, g, q0, q1);
+              else fin = pre_exec<F>(S, PrePairs{kAllLds ? lds : S.pre}, T, o, d, 1e-3f, g, q0, q1);
+            }
             GS_ADD(kGsCycRare, GS_NOW() - gs_c);
             GS_ADD(kGsRareSteps, run_rare);
             if (fin) tstate = kPending;
@@ -925,7 +970,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
           GS_ADD(kGsRecords, 1);  // (per lane: summed over every lane at the end)
           GS_ADD(kGsWeighted, (code & code_weighted) != 0);
           GS_ADD(kGsW2, (code & code_weighted) != 0 && w == 2.0f);
-          rec_push(P, code, albedo, w, V.xrec + rec0, V.xw + rec0);
+          rec_push(P, code, albedo, w, V.xrec + rec0, V.xw + rec0, rec_stride);
           o = r.p;
           d = dir;
           depth--;
@@ -956,7 +1001,7 @@ __device__ void render_general(const GeneralView &V, uint8_t *__restrict__ out, 
       GS_ADD(kGsExplicit, P.xst.n);
     }
 #endif
-    const f3 c = rec_fold(P, tail, solid_color, V.xrec + rec0, V.xw + rec0);
+    const f3 c = rec_fold(P, tail, solid_color, V.xrec + rec0, V.xw + rec0, rec_stride);
     acc = add(acc, c);
     s++;
     GS_ADD(kGsCycFold, GS_NOW() - gs_c);

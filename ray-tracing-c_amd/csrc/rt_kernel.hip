@@ -658,15 +658,15 @@ static int env_int(const char *name, int dflt) {
   const char *e = getenv(name);
   return (e && *e) ? atoi(e) : dflt;
 }
-static float env_float(const char *name, float dflt) {
+[[maybe_unused]] static float env_float(const char *name, float dflt) {
   const char *e = getenv(name);
   return (e && *e) ? (float)atof(e) : dflt;
 }
 
 enum : int { kModeLane = 0, kModeChain = 2, kModeAuto = 3 };
 
-// Every knob, read once per scene upload (INTEGRATION.md lists them): the product library reads the
-// planner / scheduling parameters only; the diagnostic build (-DRT_DIAG) also the A/B switches.
+// Every knob, read once per scene upload (INTEGRATION.md lists them): the diagnostic build (-DRT_DIAG)
+// only; the product library runs the defaults below (since r06: DESIGN.md §5.4).
 struct Config {
   bool book1 = true, book1_lds = true, general = true, gen_pre = true;
   bool lpt = true, bf = true, bf_cuts = true, px_time = false, debug = false;
@@ -680,19 +680,20 @@ struct Config {
   // 302-311, 32 304-307, 64 293-300).  RT_LPT_SPP sets both.
   int chain_pre_spp = 64;
   int mode = kModeAuto;
-  // chain_beta: a lane chain's latency target as a fraction of the launch's throughput time; 0 = by
-  // the launch's occupancy: 0.9 at 5 waves per SIMD (N = 1: fewer splits, same box 244.6-245.2 vs
-  // 246.6-247.8 ms at 0.7, 1.0 mixed), 0.7 at 3 (the shares: N = 4 95.2-96.1 ms at 0.7 vs 98.4-102.5 at
-  // 0.9, N = 8 the same within noise)
+  // chain_beta: a lane chain's latency target as a fraction of the launch's throughput time; 0 = by the
+  // launch's class (launch_chain, kTailPx): 0.7 for 0.5-2 pixels per lane of the 5-wave grid -- the N = 2 / 4
+  // shares (N = 4 95.2-96.1 ms at 0.7 vs 98.4-102.5 at 0.9) --, else 0.9 (N = 1: fewer splits, same box
+  // 244.6-245.2 vs 246.6-247.8 ms at 0.7, 1.0 mixed; N = 8 the same within noise)
   float chain_beta = 0.0f, chain_margin = 1e9f;
-  // chain_alpha: tail shaping of the plan (ChainModel.alpha; < 0: by occupancy, kTailAlpha3 at 3 waves per
-  // SIMD, off at 5); chain_floor: its smallest lane chain target, a fraction of the throughput time
+  // chain_alpha: tail shaping of the plan (ChainModel.alpha; < 0: by the launch's class, kTailAlpha for
+  // 0.5-2 pixels per lane, off otherwise); chain_floor: its smallest lane chain target, a fraction of the
+  // throughput time
   float chain_alpha = -1.0f, chain_floor = 0.1f;  // margin: records per segment / (spp / K); >= K: spp
   int chain_kmax = 32, chain_kmax_wave = 8, chain_min_seg = 16, chain_slack = 64, chain_smooth = 4;
   float chain_est = 1.0f;
   // chain_cover: pixels of >= chain_cover_k segments get segments up to max(own, estimate) x this (0: off);
-  // chain_heavy: lane pixels of >= chain_heavy_k segments get this x as many (< 1: by occupancy, kHeavy3 at 3
-  // waves per SIMD, off at 5; 1: off)
+  // chain_heavy: lane pixels of >= chain_heavy_k segments get this x as many (< 1: by the launch's class,
+  // kHeavy for the rank shares -- < 2 pixels per lane --, off for the one-GPU frame; 1: off)
   float chain_cover = 1.1f;
   int chain_cover_k = 8;
   float chain_heavy = -1.0f;
@@ -728,7 +729,10 @@ struct Config {
   float chain_occ_px = 2.0f;  // launches of fewer pixels per lane of the 5-wave grid are rank shares (kTailPx)
   static Config from_env() {
     Config c;
-    // the documented planner / scheduling parameters
+#ifdef RT_DIAG
+    // The product library reads none of these: its plan follows the launch's class alone (launch_chain,
+    // kTailPx).  The diagnostic build (librtc_amd_diag.so, -DRT_DIAG) reads the planner /
+    // scheduling parameters measured in DESIGN.md ...
     c.lpt_spp = env_int("RT_LPT_SPP", c.lpt_spp);
     if (c.lpt_spp < 1) c.lpt_spp = 1;
     if (getenv("RT_LPT_SPP")) c.chain_pre_spp = c.lpt_spp;
@@ -751,9 +755,8 @@ struct Config {
     if (c.mig_sleep < 1) c.mig_sleep = 1;
     c.mig_wait_us = env_int("RT_MIG_WAIT_US", c.mig_wait_us);
     if (c.mig_wait_us < 0) c.mig_wait_us = 0;
-#ifdef RT_DIAG
-    // the diagnostic build only (librtc_amd_diag.so, -DRT_DIAG): path selection for tests, A/B
-    // switches of the measured alternatives, timelines, fault injection
+    // ... and path selection for tests, the A/B switches of the measured alternatives, timelines, fault
+    // injection
     c.mig_drop = env_int("RT_FAULT_MIG_DROP", 0);
     if (c.mig_drop < 0) c.mig_drop = 0;
     c.cost_budget = env_int("RT_COST_BUDGET", c.cost_budget);
@@ -1221,7 +1224,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   if (cfg.pre_resume) HIP_OK(hipMalloc(&d->pre_state, npix * sizeof(float4)));
   V.pre_state = nullptr;  // (set per launch: the cost pass writes it, the chain launch after it reads it)
   if (cfg.px_time) {
-    HIP_OK(hipMalloc(&d->px_time, npix * 3 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d->px_time, npix * b1::kTimeWords * sizeof(uint32_t)));
     V.px_time = d->px_time;
   }
 #ifdef RT_LOOP_STATS
@@ -1252,7 +1255,7 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_acc0 = (float4 *)(c + co[7]);
     d->ch_cont = (b1::ChainCont *)(c + co[8]);
     if (cfg.px_time) {
-      HIP_OK(hipMalloc(&d->seg_time, nseg * 3 * sizeof(uint32_t)));
+      HIP_OK(hipMalloc(&d->seg_time, nseg * b1::kTimeWords * sizeof(uint32_t)));
       V.seg_time = d->seg_time;
     }
   }
@@ -1551,9 +1554,12 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   d->chain_occ = chain_occupancy(d, npix);
   d->chain_grid = d->chain_occ == 5 ? d->chain_grid5 : d->chain_grid3;
   if (d->px_time) {  // (diagnostic timelines: a fresh record per launch)
-    HIP_OK(hipMemsetAsync(d->px_time, 0, (size_t)d->width * d->height * 3 * sizeof(uint32_t), st));
-    HIP_OK(hipMemsetAsync(d->seg_time, 0, (size_t)d->ch_seg_cap * 3 * sizeof(uint32_t), st));
+    HIP_OK(hipMemsetAsync(d->px_time, 0, (size_t)d->width * d->height * b1::kTimeWords * sizeof(uint32_t), st));
+    HIP_OK(hipMemsetAsync(d->seg_time, 0, (size_t)d->ch_seg_cap * b1::kTimeWords * sizeof(uint32_t), st));
   }
+  // (every chain launch runs its cost pre-pass: it sets the previous launch's reservation back to kRecFill,
+  // and chain_fill_kernel below fills only what lies past the clean high-water mark -- a chain launch
+  // without this pre-pass would read the previous launch's records)
   launch_cost_pass(d, V, d_out, st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d->lpt_hist, 0, kLptHistBytes, st));
@@ -2264,7 +2270,7 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   std::vector<uint2> items(n_items);
   std::vector<b1::ChainPx> px(npix);
   std::vector<uint64_t> seg(n_seg);
-  std::vector<uint32_t> pt(3 * npix), sgt(3 * n_seg), draws(npix), costs(npix), own(npix);
+  std::vector<uint32_t> pt(b1::kTimeWords * npix), sgt(b1::kTimeWords * n_seg), draws(npix), costs(npix), own(npix);
   HIP_OK(hipMemcpy(draws.data(), d->draw_out, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(costs.data(), d->lpt_cost, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
   // (cost smoothing on: lpt_cost holds the planner's max(own, row mean); the pixel's own is cost_own)
@@ -2272,8 +2278,8 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
   HIP_OK(hipMemcpy(items.data(), d->ch_items, n_items * sizeof(uint2), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(px.data(), d->ch_px, npix * sizeof(b1::ChainPx), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(seg.data(), d->ch_seg, n_seg * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(pt.data(), d->px_time, 3 * npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(sgt.data(), d->seg_time, 3 * n_seg * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(pt.data(), d->px_time, b1::kTimeWords * npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(sgt.data(), d->seg_time, b1::kTimeWords * n_seg * sizeof(uint32_t), hipMemcpyDeviceToHost));
   const uint32_t spp = (uint32_t)d->view.cam.spp;
   for (size_t k = 0; k < n_items && (int64_t)k < max_rows; k++) {
     const uint32_t p = items[k].x, sg = items[k].y;
@@ -2283,17 +2289,18 @@ extern "C" int64_t rt_scene_chain_diag(rt_device_scene *d, uint32_t *rows, int64
     r[8] = r[9] = r[10] = 0u;
     r[11] = draws[p];
     r[12] = own[p];
-    r[13] = r[15] = 0u;
+    r[13] = r[15] = 0u;  // (15: where the item started, b1::hw_where)
     r[14] = costs[p];
     if (sg & b1::kItemUnsplit) {
-      r[1] = 0, r[2] = 1, r[4] = pt[3 * p], r[5] = pt[3 * p + 1], r[6] = spp, r[7] = 2u, r[13] = pt[3 * p + 2];
+      r[1] = 0, r[2] = 1, r[4] = pt[4 * p], r[5] = pt[4 * p + 1], r[6] = spp, r[7] = 2u, r[13] = pt[4 * p + 2], r[15] = pt[4 * p + 3];
     } else {
       const b1::ChainPx &P = px[p];
       const uint64_t w = P.end0 + sg < n_seg ? seg[P.end0 + sg] : 0ull;
       r[1] = sg, r[2] = P.K;
-      r[4] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg)] : 0u;
-      r[5] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg) + 1] : 0u;
-      r[13] = P.end0 + sg < n_seg ? sgt[3 * (P.end0 + sg) + 2] : 0u;
+      r[4] = P.end0 + sg < n_seg ? sgt[4 * (P.end0 + sg)] : 0u;
+      r[5] = P.end0 + sg < n_seg ? sgt[4 * (P.end0 + sg) + 1] : 0u;
+      r[13] = P.end0 + sg < n_seg ? sgt[4 * (P.end0 + sg) + 2] : 0u;
+      r[15] = P.end0 + sg < n_seg ? sgt[4 * (P.end0 + sg) + 3] : 0u;
       r[6] = b1::end_n(w);
       r[7] = ((w & b1::kEndEnded) && !(w & b1::kEndNoLink) ? 1u : 0u) | ((w & b1::kEndEnded) ? 2u : 0u);
       r[8] = b1::end_t(w), r[9] = b1::end_c(w), r[10] = P.seg_len;

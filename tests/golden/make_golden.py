@@ -48,7 +48,8 @@ SMALL = [
     ("s7_400x400_16spp_d50", 7, 400, 16, 50, False),
 ]
 BIG = [("s1_1200x675_1000spp_d50", 1, 1200, 1000, 50, False),  # the north-star frame (config 3/4)
-       ("s7_1000x1000_1000spp_d50", 7, 1000, 1000, 50, False)]  # config 5 at full size (~35 min, 8 cores)
+       ("s7_1000x1000_1000spp_d50", 7, 1000, 1000, 50, False),  # config 5 at full size (~35 min, 8 cores)
+       ("s1_800x450_1000spp_d50", 1, 800, 1000, 50, False)]  # another resolution of the headline (r06, ~4 min)
 
 
 def crops(img, w, h, n=8, size=32):

@@ -62,6 +62,16 @@ def test_gpu_north_star_frame_pixel_identical(manifest):
         pytest.fail(f"full-frame sha mismatch; crops differing: {bad}")
 
 
+def test_gpu_headline_scene_other_resolution(manifest):
+    """The headline scene at another resolution (800x450, 1000 spp: 0.44 M pixels, which the planner runs
+    in the class of an N = 2 share) is the reference frame (r06 generalisation check)."""
+    e = manifest["renders"].get("s1_800x450_1000spp_d50")
+    if e is None:
+        pytest.skip("golden not generated (make_golden.py --only s1_800x450_1000spp_d50)")
+    img = rtc.render(rtc.Scene.preset(1, 800, 1000, 50))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == e["sha256"]
+
+
 @pytest.mark.parametrize("world", [8, 4, 2])
 def test_gpu_north_star_rank_shares_reassemble(manifest, world):
     """BASELINE config 4 (the north-star frame over 8 GPUs, rows j % 8) rehearsed on one device:
