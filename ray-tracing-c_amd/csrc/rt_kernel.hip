@@ -285,6 +285,11 @@ constexpr float kTailAlpha = 1.5f, kTailPx = 0.5f;
 // max rank ms, two rounds (3 waves): off 60.9 / 60.5, 1.5: 60.7 / 59.7, 2: 59.7 / 59.4, 2 from 4 segments:
 // 64.6 / 64.1; N = 2 unchanged (147-148).
 constexpr float kHeavy = 2.0f;
+// Tail migration (rt_book1.h: MigRec): a drained wave hands its chains to helper waves once at most this many
+// of its lanes are live (and 70 % of the grid's waves have finished).  The one-GPU frame: 48 (r06, same box,
+// two rounds, Msamples/s: 16 3358 / 3364, 32 3389 / 3391, 48 3419 / 3406, 63 3414 / 3380); the rank shares:
+// 16 (N = 8 max rank ms: 63 60.5 vs 52.3, r05 32 55.0 vs 54.3).
+constexpr int kMigLive = 48, kMigLiveShare = 16;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
@@ -705,7 +710,8 @@ struct Config {
   int gen_batch = 56, gen_steps = 16, gen_lds = 1024, gen_rare = 8, gen_flat = 3;
   bool gen_big = true;  // general path: whole preorder in one 768-thread workgroup's LDS when it fits
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
-  int mig_live = 16;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
+  int mig_live = -1;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
+                      //   (< 0: by the launch's class, kMigLive / kMigLiveShare; 0: off)
   int mig_idle = 70;  //   ... once this percentage of the grid's waves has finished (50 until r05: same box, three
                       //   rounds, N = 1 frame kernel p50 230.3-231.9 ms at 70 vs 231.8-232.8; N = 2 142.0 / 142.1
                       //   vs 143.4 / 143.7, N = 8 equal; 85-90 slower)
@@ -745,7 +751,7 @@ struct Config {
     c.chain_cover_k = env_int("RT_CHAIN_COVER_K", c.chain_cover_k);
     c.chain_heavy_k = env_int("RT_CHAIN_HEAVY_K", c.chain_heavy_k);
     c.mig_live = env_int("RT_MIG_LIVE", c.mig_live);
-    c.mig_live = c.mig_live < 0 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
+    c.mig_live = c.mig_live < -1 ? 0 : (c.mig_live > 63 ? 63 : c.mig_live);
     c.mig_idle = env_int("RT_MIG_IDLE", c.mig_idle);
     c.mig_poll_us = env_int("RT_MIG_POLL_US", c.mig_poll_us);
     c.chain_walk = env_int("RT_CHAIN_WALK", c.chain_walk);
@@ -1199,8 +1205,8 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
   V.mats = (const b1::FastMat *)(b + off[1]);
   V.work_counter = (int32_t *)(b + off[2]);  // (the counter; the migration words from the next line on)
   V.mig = (uint32_t *)(b + off[2] + 128);
-  V.mig_live = cfg.mig_live;
-  if (cfg.mig_live > 0) {  // one queue entry per lane of the grid: an item migrates at most once per launch...
+  V.mig_live = cfg.mig_live < 0 ? kMigLiveShare : cfg.mig_live;  // (launch_chain sets it by the launch's class)
+  if (cfg.mig_live != 0) {  // one queue entry per lane of the grid: an item migrates at most once per launch...
     V.mig_cap = (uint32_t)spill_lanes;  // ...and only against an idle helper wave (push beyond: the lane keeps it)
     HIP_OK(hipMalloc(&d->mig_q, (size_t)V.mig_cap * sizeof(b1::MigRec)));
     HIP_OK(hipMemset(d->mig_q, 0, (size_t)V.mig_cap * sizeof(b1::MigRec)));  // epoch 0: no entry
@@ -1591,6 +1597,7 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   m.cover = cfg.chain_cover;
   m.cover_k = cfg.chain_cover_k < 2 ? 2 : cfg.chain_cover_k;
   m.heavy = cfg.chain_heavy >= 1.0f ? cfg.chain_heavy : (share ? kHeavy : 1.0f);
+  if (cfg.mig_live < 0) V.mig_live = share ? kMigLiveShare : kMigLive;
   m.heavy_k = cfg.chain_heavy_k < 2 ? 2 : cfg.chain_heavy_k;
   m.pad_k = cfg.chain_pad_k < 2 ? 2 : cfg.chain_pad_k;
   m.kmax_lane = cfg.chain_kmax;
