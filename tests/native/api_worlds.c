@@ -23,7 +23,7 @@
  *  10 1000 boxes (6000 quads) in a BVH under a sampled light: ~7000 preorder entries (220 KiB) exceed
  *     one workgroup's 160 KiB of LDS, so the general path runs its 256-thread kernel with the first
  *     entries in LDS and the rest in global memory
- * usage: api_worlds <id> <out.rgb>     prints "width height" on stdout */
+ * usage: see main()     prints "width height" on stdout per frame */
 #include "hittable.h"
 #include "material.h"
 #include "pcg32.h"
@@ -228,15 +228,11 @@ static void world_many_boxes(World *w, Camera *c) {
   HittableList_append(&w->lights, panel);
 }
 
-int main(int argc, char **argv) {
-  if (argc < 3) {
-    fprintf(stderr, "usage: %s <world 0-10> <out.rgb>\n", argv[0]);
-    return 2;
-  }
+static int render_world(int id, const char *path) {
   World world;
   World_init(&world, 256);
   Camera camera;
-  switch (atoi(argv[1])) {
+  switch (id) {
     case 0: world_surface_normal(&world, &camera); break;
     case 1: world_hollow_glass(&world, &camera); break;
     case 2: world_metal_fuzz(&world, &camera); break;
@@ -255,12 +251,34 @@ int main(int argc, char **argv) {
   uint8_t *img = malloc(n);
   Camera_render(&camera, &world, img);
   report_kernel(&camera, &world);
-  FILE *f = fopen(argv[2], "wb");
+  FILE *f = fopen(path, "wb");
   if (!f || fwrite(img, 1, n, f) != n) {
-    fprintf(stderr, "cannot write %s\n", argv[2]);
+    fprintf(stderr, "cannot write %s\n", path);
     return 1;
   }
   fclose(f);
+  free(img);
   printf("%d %d\n", camera.img_width, camera.img_height);
   return 0;
+}
+
+/* usage: api_worlds <id> <out.rgb>
+ *        api_worlds seq <out_prefix> <id> <id> ...   several worlds, each built afresh and rendered by
+ *        Camera_render in this one process, into <out_prefix>_<k>.rgb (k = position in the list): a
+ *        repeated world reuses the drop-in library's cached device scene, a different one replaces it */
+int main(int argc, char **argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s <world 0-10> <out.rgb> | seq <out_prefix> <world> ...\n", argv[0]);
+    return 2;
+  }
+  if (argv[1][0] == 's') {
+    char path[4096];
+    for (int k = 3; k < argc; k++) {
+      snprintf(path, sizeof path, "%s_%d.rgb", argv[2], k - 3);
+      const int rc = render_world(atoi(argv[k]), path);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  return render_world(atoi(argv[1]), argv[2]);
 }

@@ -21,6 +21,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden", "api")
 EXE = os.path.join(ROOT, "tests", "native", "bin", "api_worlds_gpu")
+# the same source linked to the diagnostic build (librtc_amd_diag.so): the product ignores path switches
+EXE_DIAG = os.path.join(ROOT, "tests", "native", "bin", "api_worlds_gpu_diag")
 MAN = json.load(open(os.path.join(GOLD, "manifest.json")))
 WORLDS = sorted(MAN["worlds"], key=int)
 # worlds the Book-1 fast path takes (spheres, Solid Lambertian / Metal / Dielectric, max_depth <= 64)
@@ -43,9 +45,9 @@ def test_api_worlds_binary_built():
     assert os.access(EXE, os.X_OK), "make -C tests/native"
 
 
-def _render(wid, tmp_path, env=None, kernel=False):
+def _render(wid, tmp_path, env=None, kernel=False, exe=EXE):
     out = tmp_path / f"w{wid}.rgb"
-    r = subprocess.run([EXE, wid, str(out)], capture_output=True, text=True, timeout=120,
+    r = subprocess.run([exe, wid, str(out)], capture_output=True, text=True, timeout=120,
                        env={**os.environ, **(env or {}), **({"API_WORLDS_KERNEL": "1"} if kernel else {})})
     assert r.returncode == 0, r.stderr[-2000:]
     w, h = (int(x) for x in r.stdout.split())
@@ -76,8 +78,34 @@ def test_gpu_api_world_matches_reference_build(wid, tmp_path):
 @pytest.mark.parametrize("env", [{"RT_MODE": "lane"}, {"RT_MODE": "chain", "RT_LPT_SPP": "2"}, {"RT_BOOK1": "0"}])
 @pytest.mark.parametrize("wid", BOOK1)
 def test_gpu_api_world_book1_variants(wid, env, tmp_path):
+    """The Book-1 worlds forced onto the lane kernel, the chain kernel and the general kernel (the
+    diagnostic build's path switches; the product library ignores them): each the reference's frame, and
+    the kernel the library picked is the one forced."""
     ref, e = golden(wid)
-    _check(_render(wid, tmp_path, env), ref, f"world {wid} ({e['name']}) {env}")
+    img, kernel = _render(wid, tmp_path, env, kernel=True, exe=EXE_DIAG)
+    # (RT_MODE=chain falls back to the lane kernel where a chain launch does not apply: < 4096 pixels or spp
+    # below 4 x the pre-pass's)
+    want = {"lane": ("rt_book1_kernel<",), "chain": ("rt_book1_chain_kernel<", "rt_book1_kernel<")}.get(
+        env.get("RT_MODE"), ("rt_general_kernel<",))
+    assert kernel is not None and kernel.startswith(want), f"world {wid} {env}: picked {kernel}"
+    _check(img, ref, f"world {wid} ({e['name']}) {env}")
+
+
+@pytest.mark.gpu
+def test_gpu_api_worlds_in_one_process(tmp_path):
+    """Several worlds built afresh and rendered by Camera_render in one process (api_worlds seq): the
+    drop-in library's device-scene cache reuses a scene only when the flattened world,
+    camera and environment are byte-identical -- alternating worlds and repeating one must each give that
+    world's reference frame."""
+    seq = ["6", "2", "6", "6", "1", "2"]
+    r = subprocess.run([EXE, "seq", str(tmp_path / "f")] + seq, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    dims = [tuple(int(x) for x in ln.split()) for ln in r.stdout.splitlines()]
+    assert len(dims) == len(seq)
+    for k, (wid, (w, h)) in enumerate(zip(seq, dims)):
+        ref, e = golden(wid)
+        img = np.fromfile(tmp_path / f"f_{k}.rgb", np.uint8).reshape(h, w, 3)
+        _check(img, ref, f"call {k}: world {wid} ({e['name']})")
 
 
 # The product library's size-driven fallbacks, reached with librtc_amd.so (no diagnostic build, no
