@@ -41,7 +41,7 @@ PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFM
 ISSUE_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # committed rocprofv3 PMC summaries, one per configuration (scripts/gpu_profile.sh -> scripts/pmc_summary.py):
 # profiles/<round>/pmc_<config key>.json, stamped with the build id of the library they measured
-PMC_DIR = os.path.join(ROOT, "profiles", "r05")
+PMC_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def parse():

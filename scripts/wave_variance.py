@@ -13,7 +13,7 @@ hw = rows[:,15]
 xcc = hw>>28; h=hw&0xffff
 wid = h&15; simd=(h>>4)&3; cu=(h>>8)&15; sh=(h>>12)&1; se=(h>>13)&7
 print("xcc", np.unique(xcc), "se", np.unique(se), "sh", np.unique(sh), "cu", np.unique(cu), "simd", np.unique(simd), "wave ids", np.unique(wid)[:20])
-m = (wave==0)&(rows[:,13]==0)&(recs>20)&(start<3)
+m = (wave==0)&(rows[:,13]==0)&(recs>20)&(start<3)&(seg>0)&(K>1)  # segments k >= 1 only: their records are all rendered in the launch (segment 0 and unsplit items also count the pre-pass samples they resumed)
 sps = rows[:,12]/64.0
 lat = dur/np.maximum(recs,1)*1e3
 # predicted: median lat in sps bins
