@@ -872,7 +872,8 @@ struct rt_device_scene {
   b1::ChainCont *ch_cont = nullptr;
   uint32_t ch_seg_cap = 0;
   void *ch_rec_arena = nullptr;
-  size_t ch_rec_cap = 0;  // records
+  size_t ch_rec_cap = 0;     // records
+  size_t ch_rec_demand = 0;  // records the last chain launch wanted (read back after rt_render_share's launches)
   // general path (rt_general.h) for scenes outside the Book-1 path
   bool general = false;
   void *gen_arena = nullptr;
@@ -1505,14 +1506,31 @@ static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V
   else hipLaunchKernelGGL((rt_book1_chain_kernel<false>), gc, blk, 0, st, V, d_out);
 }
 
-// Records of a chain launch: grown on demand, up to the RT_CHAIN_MB budget (the planner keeps
-// pixels whole when they run out).
+// Records of a chain launch, up to the RT_CHAIN_MB budget (the planner keeps pixels whole when they run out).
+// The plan reserves spp + slack records for every segment past a pixel's first, and a launch's segments number
+// at most (kmin - 1) x npix + about 1.5 x lanes (the fill to one item per lane, then c* = beta T: a lane's worth
+// of cost per segment).  Measured reservations of the headline frame: 0.16 / 7.4 / 9.0 / 6.1 GB at N = 1 / 2 / 4
+// / 8, against 8.4 / 8.4 / 11.8 / 13.5 GB of that bound; until r06 the arena took the whole
+// 24-GiB budget, which every cached scene then held and every cold call allocated and freed.  A launch that
+// wanted more than the arena held (ch_rec_demand, read back by rt_render_share after its launch) grows the
+// next one's.  Small launches (worst case <= 4 GiB) get the worst case: every pixel split as far as allowed.
 static int chain_records(rt_device_scene *d, size_t npix, int spp, hipStream_t st) {
   const Config &cfg = d->cfg;
   const size_t kmax = (size_t)(cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave);
   const double seg_recs = fmin((double)cfg.chain_margin * spp / 2.0, (double)spp) + cfg.chain_slack;
   const size_t per_px = (size_t)ceil((double)(kmax - 1) * seg_recs) + (size_t)spp + (size_t)cfg.chain_slack;
-  size_t want = npix * per_px;
+  size_t want = npix * per_px;  // the worst case
+  const size_t small = ((size_t)4 << 30) / sizeof(float4);
+  if (want > small) {
+    const double lanes = (double)d->chain_grid5 * b1::kBlock;
+    const double kmin = cfg.chain_fill > 0.0f ? ceil(lanes * cfg.chain_fill / (double)npix) : 1.0;
+    const double segs = (kmin > 1.0 ? kmin - 1.0 : 0.0) * (double)npix + 1.5 * lanes;
+    size_t bound = (size_t)(segs * ((double)spp + cfg.chain_slack)) + (size_t)spp + (size_t)cfg.chain_slack;
+    const size_t grow = d->ch_rec_demand + d->ch_rec_demand / 4;
+    if (bound < grow) bound = grow;
+    if (bound < small) bound = small;
+    if (want > bound) want = bound;
+  }
   const size_t budget = cfg.chain_mb * ((size_t)1 << 20) / sizeof(float4);
   if (want > budget) want = budget;
   if (want > 0xfff00000u) want = 0xfff00000u;  // u32 record indices
@@ -2144,6 +2162,11 @@ static int render_share(const rt_flat_scene *s, const std::function<const HostPa
       rc = -1;
     } else if (rt_scene_check(e->scene) != 0) {  // never a partial image with rc 0
       rc = -1;
+    } else if (e->scene->ch_cnt) {  // the records the launch's plan wanted: a kept scene's next arena
+      unsigned long long want = 0;
+      if (hipMemcpy(&want, e->scene->ch_cnt + kCnRec, sizeof want, hipMemcpyDeviceToHost) == hipSuccess &&
+          want > e->scene->ch_rec_cap)
+        e->scene->ch_rec_demand = (size_t)want;
     }
   }
   if (rc == 0) {
