@@ -24,6 +24,8 @@ struct Item {
   int sphere;
 };
 
+static long dq_ref_steps, dq_steps, dq_rollbacks;  // (the deferred trace's counters, below)
+
 struct Ray {
   float o[3], d[3], inv[3], a;
 };
@@ -110,7 +112,7 @@ static bool sphere_ref(const Item &it, const Ray &R, float tmin, float tmax, flo
 static void trace_ref(const std::vector<Item> &items, const Ray &R, float tmin, float *t, int *hit) {
   float tmax = INFINITY;
   *hit = -1;
-  for (size_t p = 0; p < items.size();) {
+  for (size_t p = 0; p < items.size(); dq_ref_steps++) {
     const Item &it = items[p];
     if (it.leaf) {
       float r;
@@ -312,6 +314,51 @@ static void set_ray(Ray &R, const float o[3], const float d[3]) {
   R.a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
 }
 
+// The deferred sphere tests tried in r06 (profiles/r06/leaf_defer_experiment.patch: trav_step_defer / defer_drain):
+// a leaf waits in the lane's one slot while the walk goes on over boxes with the stale t_max, until a
+// random delay of up to `window` steps runs out, the walk reaches the next leaf (that step is lost) or
+// the end; a deferred hit sends the walk back to the leaf's successor.  Must give the reference's hit
+// bit for bit under any drain schedule; counts the steps it takes against the reference scan's.
+static void trace_defer(const std::vector<Item> &items, const Ray &R, float tmin, int window, float *t, int *hit) {
+  float tmax = INFINITY;
+  *hit = -1;
+  long pend = -1;
+  int wait = 0;
+  size_t p = 0;
+  for (;;) {
+    bool drain = false;
+    if (p >= items.size()) {
+      if (pend < 0) break;
+      drain = true;
+    } else {
+      dq_steps++;
+      const Item &it = items[p];
+      if (it.leaf) {
+        if (pend >= 0) {
+          drain = true;  // blocked: the slot is taken
+        } else {
+          pend = (long)p;
+          wait = window > 0 ? (int)(frand() * (float)(window + 1)) : 0;
+          p++;
+        }
+      } else {
+        p += aabb_ref(it, R, tmin, tmax) ? 1 : it.skip;
+      }
+      if (pend >= 0 && wait-- <= 0) drain = true;
+    }
+    if (drain && pend >= 0) {
+      float r;
+      if (sphere_ref(items[pend], R, tmin, tmax, &r)) {
+        tmax = r, *hit = items[pend].sphere;
+        p = (size_t)pend + 1;
+        dq_rollbacks++;
+      }
+      pend = -1;
+    }
+  }
+  *t = tmax;
+}
+
 int main(int argc, char **argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: bf_check <scene> <width> <n_rays> <seed>\n");
@@ -329,7 +376,7 @@ int main(int argc, char **argv) {
   long w_dec = 0, w_und = 0, w_bad = 0;
   const rt_camera &c = s->camera;
   const float tmin = 1e-3f;
-  long decided = 0, undecided = 0, bad = 0, hits = 0;
+  long decided = 0, undecided = 0, bad = 0, hits = 0, d_bad = 0;
   for (long k = 0; k < n_rays;) {
     // a camera ray through a random pixel position, with the defocus disc
     const float fi = frand() * (float)c.width, fj = frand() * (float)c.height;
@@ -347,6 +394,15 @@ int main(int argc, char **argv) {
       int h_ref, h_bf;
       trace_ref(items, R, tmin, &t_ref, &h_ref);
       if (getenv("BF_CENSUS")) census(items, R, tmin);
+      if (const char *dw = getenv("BF_DEFER")) {
+        float t_d;
+        int h_d;
+        trace_defer(items, R, tmin, atoi(dw), &t_d, &h_d);
+        if (h_d != h_ref || (h_ref >= 0 && t_d != t_ref)) {
+          if (d_bad < 10) fprintf(stderr, "deferred mismatch: ref %d %a, deferred %d %a\n", h_ref, t_ref, h_d, t_d);
+          d_bad++;
+        }
+      }
       if (trace_bf(items, R, tmin, &t_bf, &h_bf)) {
         decided++;
         if (h_bf != h_ref || (h_ref >= 0 && t_bf != t_ref)) {
@@ -393,6 +449,12 @@ int main(int argc, char **argv) {
   fprintf(stderr, "wide (8-wide group trace): %s, %zu nodes; decided %ld, undecided %ld, mismatches %ld, %.2f nodes/ray\n",
           wide_ok ? "built" : "not buildable", wide.size(), w_dec, w_und, w_bad, (double)wide_iters / n_rays);
   bad += w_bad;
+  if (getenv("BF_DEFER")) {
+    fprintf(stderr, "deferred sphere tests (window %s): mismatches %ld; steps %.2f per ray against the reference scan's %.2f "
+            "(x%.3f), rollbacks %.3f per ray\n", getenv("BF_DEFER"), d_bad, (double)dq_steps / n_rays,
+            (double)dq_ref_steps / n_rays, (double)dq_steps / (double)dq_ref_steps, (double)dq_rollbacks / n_rays);
+    bad += d_bad;
+  }
   if (getenv("BF_CENSUS")) {
     fprintf(stderr, "per ray: reference scan %.1f items; t_max-free scan %.1f nodes, %.1f leaves; cut candidates",
             (double)cen_ref / n_rays, (double)cen_free_nodes / n_rays, (double)cen_free_leaves / n_rays);
