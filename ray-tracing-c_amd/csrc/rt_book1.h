@@ -1264,7 +1264,13 @@ __device__ __attribute__((noinline)) void coop_items(KernargView kv, uint8_t *__
 }
 
 enum : int { kTrav = 0, kWait = 1, kExit = 2 };
-// traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
+// Issue priority of a chain launch's lane waves by their live lanes (r06): until the work
+// items run out every wave is full (a lane that finishes an item takes the next in the same pass); after
+// that the waves that still hold the most chains -- where the launch's last ones are -- issue first on
+// their SIMD.  RT_LIVE_PRIO=0 (compile time): off, for A/B builds.
+#ifndef RT_LIVE_PRIO
+#define RT_LIVE_PRIO 1
+#endif// traversal steps per pass before the wave re-checks its shading batch (measured, N = 1 kernel:
 // 3: 384 ms, 4: 362 ms, 6: 345 ms, 8: 334 ms, 12: 330 ms, 16: 324 ms; frames identical -- the
 // schedule never changes a lane)
 constexpr int kSteps = 16;
@@ -1343,6 +1349,16 @@ __device__ void render_batched(const Book1View &V, uint8_t *__restrict__ out, ch
     // shade once shade_batch lanes wait -- or, when fewer lanes are left (the frame's tail), once
     // 3/4 of them do, so a long path is not held back behind its wave's last traversals
     const int live = (int)__popcll(trav | wait);
+#if RT_LIVE_PRIO
+    // (same box, DESIGN.md §4.1, profiles/r06/ab_live_prio.txt: 3-2-1 at 56-40-24 live lanes against none, the
+    // N = 1 chain kernel -1.5 %, the N = 8 / 4 / 2 shares' max rank -6 / -2 / -4 %; sparse waves first: slower)
+    if (kMode == 2) {
+      if (live >= 56) __builtin_amdgcn_s_setprio(3);
+      else if (live >= 40) __builtin_amdgcn_s_setprio(2);
+      else if (live >= 24) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     const int batch = min(V.shade_batch, (3 * live + 3) / 4);
     const bool do_trav = trav != 0 && (int)__popcll(wait) < batch;
 #ifdef RT_LOOP_STATS
