@@ -1169,6 +1169,9 @@ __device__ __forceinline__ const Book1View &view_of(KernargView kv) {
   return *(const Book1View *)(KernargView)(((uint64_t)hi << 32) | lo);
 }
 
+#ifndef RT_HELP_PRIO
+#define RT_HELP_PRIO 2
+#endif
 // A wave whose lanes have all finished: run the migrated items of its mailbox until every item of
 // the launch is done.
 template <int kMode, bool kLds>
@@ -1211,7 +1214,7 @@ __device__ __attribute__((noinline)) void mig_help(KernargView kv, uint8_t *__re
       if (V.mig_drop && l0) drop = atomicAdd(&V.mig[kMigDropped], 1u) < V.mig_drop;
 #endif
       if (!__builtin_amdgcn_readfirstlane(drop)) {
-        __builtin_amdgcn_s_setprio(2);  // the frame's last chains: issue ahead of the lanes' waves
+        __builtin_amdgcn_s_setprio(RT_HELP_PRIO);  // the frame's last chains: issue ahead of the lanes' waves
         render_item_coop<kMode>(V, items9, (int64_t)r.pix, r.seg, out, &r);
         __builtin_amdgcn_s_setprio(0);
         if (l0) mig_item_done(V, total_own);

@@ -286,10 +286,12 @@ constexpr float kTailAlpha = 1.5f, kTailPx = 0.5f;
 // 64.6 / 64.1; N = 2 unchanged (147-148).
 constexpr float kHeavy = 2.0f;
 // Tail migration (rt_book1.h: MigRec): a drained wave hands its chains to helper waves once at most this many
-// of its lanes are live (and 70 % of the grid's waves have finished).  The one-GPU frame: 48 (r06, same box,
-// two rounds, Msamples/s: 16 3358 / 3364, 32 3389 / 3391, 48 3419 / 3406, 63 3414 / 3380); the rank shares:
-// 16 (N = 8 max rank ms: 63 60.5 vs 52.3, r05 32 55.0 vs 54.3).
-constexpr int kMigLive = 48, kMigLiveShare = 16;
+// of its lanes are live (and 70 % of the grid's waves have finished).  The one-GPU frame: 32 since the lane
+// waves' live-lane priority (rt_book1.h RT_LIVE_PRIO; same box, two rounds, Msamples/s: 24 3480 / 3494, 32
+// 3498 / 3491, 40 3495 / 3494, 48 3471 / 3471; without the priority 48 was best: 16 3358 / 3364, 32 3389 / 3391,
+// 48 3419 / 3406, 63 3414 / 3380); the rank shares: 16 (with the priority, N = 8 / 4 / 2 max rank ms: 8 51.4 /
+// 80.7 / 135.6, 16 49.9 / 82.3 / 134.9, 24 51.3 / 83.9 / 135.8, 32 52.7 / 85.8 / 137.2).
+constexpr int kMigLive = 32, kMigLiveShare = 16;
 
 // one thread: running offsets, highest bucket first (longest first)
 __global__ void lpt_scan_kernel(uint32_t *hist) {
