@@ -714,9 +714,11 @@ struct Config {
   bool gen_perlin = true;  // ... and the Perlin tables behind it when they fit too
   int mig_live = -1;  // tail migration (rt_book1.h: MigRec): lanes left in a wave when it hands them over
                       //   (< 0: by the launch's class, kMigLive / kMigLiveShare; 0: off)
-  int mig_idle = 70;  //   ... once this percentage of the grid's waves has finished (50 until r05: same box, three
-                      //   rounds, N = 1 frame kernel p50 230.3-231.9 ms at 70 vs 231.8-232.8; N = 2 142.0 / 142.1
-                      //   vs 143.4 / 143.7, N = 8 equal; 85-90 slower)
+  int mig_idle = 30;  //   ... once this percentage of the grid's waves has finished: 30 since the live-lane priority
+                      //   (same box, two rounds, N = 1 step / N = 8 / 4 / 2 max rank ms: 70 231.3 / 50.1 / 81.8 /
+                      //   135.0, 40 231.5 / 48.8 / 80.4 / 133.9, 30 231.3 / 48.7 / 80.3 / 134.0, 20 231.0 / 49.4 /
+                      //   79.8 / 133.7, 0 231.1 / 48.8 / 79.5 / 133.5); 70 in r05-r06 before it (50 until r05: N = 1
+                      //   p50 230.3-231.9 at 70 vs 231.8-232.8, N = 2 142.0 / 142.1 vs 143.4 / 143.7, 85-90 slower)
   int mig_poll_us = 500;  //   a sparse wave's reads of the helper count until the gate opens (20 until r05:
                          //   N = 8 58.7-59.2 vs 56.0-57.2 ms, same box; 100 / 1000 / 2000 between / equal)
   int chain_blocks3 = 0;  // (diagnostic) blocks per CU of the shares' chain kernel (0: as many as fit)
