@@ -724,7 +724,10 @@ struct Config {
   int chain_blocks3 = 0;  // (diagnostic) blocks per CU of the shares' chain kernel (0: as many as fit)
   int chain_walk = 4;  // a segment past its check walks its pixel's links every this many samples (power of
                        // 2; 8 / 16 measured equal)
-  int mig_help = 40;  //   this percentage of the grid's waves stays resident as helpers
+  int mig_help = 80;  //   this percentage of the grid's waves stays resident as helpers: 80 since the live-lane
+                      //   priority and the 30-% gate (same box, two rounds each, two calls, N = 1 step / N = 8 / 4 / 2
+                      //   max rank ms: 40 230.5 / 48.6 / 80.0 / 134.0, 80 231.0 / 48.1 / 79.2 / 133.7, 100 230.4 /
+                      //   48.2 / 79.3 / 133.6); 40 before
   int mig_sleep = 64; //   helpers' poll interval (x ~3.4 us)
   int mig_wait_us = 4000000;  // a helper idle this long leaves (taking back its unclaimed credit)
   int mig_drop = 0;   // fault injection (tests only): helpers drop this many migrated items
