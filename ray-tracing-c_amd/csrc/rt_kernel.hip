@@ -881,6 +881,11 @@ struct rt_device_scene {
   void *ch_rec_arena = nullptr;
   size_t ch_rec_cap = 0;     // records
   size_t ch_rec_demand = 0;  // records the last chain launch wanted (read back after rt_render_share's launches)
+  // (every chain launch also copies its plan's reservation to pinned host memory, for the next launch on this scene
+  // to see without a host sync: rt_render_rows_async callers get the arena grown too)
+  unsigned long long *rec_demand_host = nullptr;
+  hipEvent_t ev_demand = nullptr;
+  bool demand_pending = false;
   // general path (rt_general.h) for scenes outside the Book-1 path
   bool general = false;
   void *gen_arena = nullptr;
@@ -1260,6 +1265,9 @@ static int book1_upload(rt_device_scene *d, const rt_flat_scene *s, const HostPa
     d->ch_cnt = (uint32_t *)(c + co[0]);
     d->ch_dirty = d->ch_cnt + kCnWords;  // (past the words each plan zeroes)
     HIP_OK(hipMemset(d->ch_dirty, 0, kDirtyWords * sizeof(uint32_t)));
+    HIP_OK(hipHostMalloc((void **)&d->rec_demand_host, sizeof(unsigned long long), hipHostMallocDefault));
+    *d->rec_demand_host = 0ull;
+    HIP_OK(hipEventCreateWithFlags(&d->ev_demand, hipEventDisableTiming));
     d->ch_k = (uint32_t *)(c + co[1]);
     d->ch_split = (uint32_t *)(c + co[2]);
     d->ch_px = (b1::ChainPx *)(c + co[3]);
@@ -1462,6 +1470,8 @@ extern "C" void rt_scene_release(rt_device_scene *d) {
   if (d->pre_arena) (void)hipFree(d->pre_arena);
   if (d->ch_arena) (void)hipFree(d->ch_arena);
   if (d->ch_rec_arena) (void)hipFree(d->ch_rec_arena);
+  if (d->rec_demand_host) (void)hipHostFree(d->rec_demand_host);
+  if (d->ev_demand) (void)hipEventDestroy(d->ev_demand);
   if (d->status) (void)hipFree(d->status);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
   for (hipEvent_t e : d->ev_main)
@@ -1523,6 +1533,13 @@ static void launch_chain_kernel(const rt_device_scene *d, const b1::Book1View &V
 // next one's.  Small launches (worst case <= 4 GiB) get the worst case: every pixel split as far as allowed.
 static int chain_records(rt_device_scene *d, size_t npix, int spp, hipStream_t st) {
   const Config &cfg = d->cfg;
+  // the reservation a previous launch's plan wanted, if its copy has landed (queried, never waited on: the
+  // launch stays asynchronous; a launch enqueued before it lands is planned on the old arena)
+  if (d->demand_pending && hipEventQuery(d->ev_demand) == hipSuccess) {
+    d->demand_pending = false;
+    const size_t want = (size_t)*d->rec_demand_host;
+    if (want > d->ch_rec_cap && want > d->ch_rec_demand) d->ch_rec_demand = want;
+  }
   const size_t kmax = (size_t)(cfg.chain_kmax > cfg.chain_kmax_wave ? cfg.chain_kmax : cfg.chain_kmax_wave);
   const double seg_recs = fmin((double)cfg.chain_margin * spp / 2.0, (double)spp) + cfg.chain_slack;
   const size_t per_px = (size_t)ceil((double)(kmax - 1) * seg_recs) + (size_t)spp + (size_t)cfg.chain_slack;
@@ -1650,6 +1667,11 @@ static int launch_chain(rt_device_scene *d, b1::Book1View V, uint8_t *d_out, hip
   hipLaunchKernelGGL(chain_dirty_kernel, dim3(1), dim3(64), 0, st, d->ch_cnt, d->ch_dirty, (uint32_t)d->ch_rec_cap);
   hipLaunchKernelGGL(chain_fill_kernel, dim3(2048), dim3(256), 0, st, col, (const uint32_t *)d->ch_dirty);
   HIP_OK(hipGetLastError());
+  if (d->rec_demand_host && !d->demand_pending) {  // (the plan's reservation, for the next launch's arena: above)
+    HIP_OK(hipMemcpyAsync(d->rec_demand_host, d->ch_cnt + kCnRec, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(d->ev_demand, st));
+    d->demand_pending = true;
+  }
   if (cfg.debug) {  // diagnostic: synchronous peek at the plan
     uint32_t c[16];
     HIP_OK(hipStreamSynchronize(st));

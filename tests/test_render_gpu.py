@@ -367,6 +367,34 @@ def test_bench_two_rank_launch_reassembles_reference_frame():
     assert line["parity"]["max_abs_pixel_diff"] == 0
 
 
+def test_record_arena_grows_for_async_launches(monkeypatch):
+    """A plan that wants more records than the arena's bound holds keeps its excess pixels whole (exact, but a
+    whole 1000-sample chain per lane: ~3x slower).  rt_render_share grows the next arena from a synchronous
+    read-back; rt_render_rows_async (DeviceScene, bench.py) from the plan's reservation copied to pinned memory
+    and read by the next launch once it has landed.  Forced here with a tail-shaping alpha of 1.0 on an N = 4
+    share of the headline frame (its plan wants ~795 M records against a bound of ~739 M): the launches after the
+    first must run on a grown arena -- several times faster -- with the same rows."""
+    import torch
+
+    monkeypatch.setenv("RT_CHAIN_ALPHA", "1.0")
+    with rtc.use_diag():
+        sc = rtc.Scene.preset(1, 1200, 1000, 50)
+        ds = rtc.DeviceScene(sc, 0)
+    stream = torch.cuda.current_stream(0)
+    row0, stride, n = rtc.rows_of(sc.height, 0, 4)
+    ms, rows = [], []
+    for _ in range(3):
+        buf = torch.empty((n, sc.width, 3), dtype=torch.uint8, device="cuda:0")
+        ds.render_rows_async(row0, stride, n, buf.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        ds.check()
+        ms.append(ds.last_launch_ms())
+        rows.append(buf.cpu().numpy())
+    ds.close()
+    assert all((r == rows[0]).all() for r in rows[1:])
+    assert ms[2] < 0.6 * ms[0], ms
+
+
 # Tail migration (rt_book1.h: MigRec) forced onto every wave that runs out of work: any wave with
 # live lanes and no items left hands them to helpers, every finished wave stays a helper.
 MIGRATE = {**CHAIN, "RT_CHAIN_BETA": "0.001", "RT_MIG_LIVE": "63", "RT_MIG_IDLE": "0", "RT_MIG_HELP": "100"}
