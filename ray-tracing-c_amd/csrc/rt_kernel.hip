@@ -277,8 +277,13 @@ constexpr float kLaneLat = 1900.0f, kLaneThr = 2714.0f, kCoopStep = 250.0f;
 // Tail shaping (ChainModel.alpha) for the N = 2 / 4 shares.  Same box, max rank ms, three rounds, r05 at 3
 // waves: N = 2 alpha 0: 164.4-167.1, 1.5: 150.7-153.4, 2: 162.3-165.1, 3: 167.1-169.6; N = 4
 // 0: 94.0-95.3, 1.5: 93.5-94.5; N = 8 (two rounds) 0: 61.0-61.3, 1.5: 62.4-63.1 (5 waves: 60.1 / 60.0 vs
-// 55.0 / 55.0); N = 1 1.5: 257.6-258.4 vs 252.0-252.8 ms per frame.
-constexpr float kTailAlpha = 1.5f, kTailPx = 0.5f;
+// 55.0 / 55.0); N = 1 1.5: 257.6-258.4 vs 252.0-252.8 ms per frame.  With r06's live-lane priority (the fullest
+// waves issue first) the optimum moved to 2 (same box, two rounds, N = 4 / 2 max rank ms: 1.5 79.1 / 79.9 and 133.7 /
+// 133.7; 2 77.7 / 77.8 and 130.4 / 129.5; 2.5 77.5 / 77.4 and 131.6 / 132.2; profiles/r06/sweep_alpha_r06.txt).
+#ifndef RT_TAIL_ALPHA
+#define RT_TAIL_ALPHA 2.0f
+#endif
+constexpr float kTailAlpha = RT_TAIL_ALPHA, kTailPx = 0.5f;
 // Heavy pixels (ChainModel.heavy) in the shares: a pixel planned at >= 8 lane segments gets twice as many.
 // Its waves hold only heavy lanes (image-tile order) and run up to 3x slower per traversal step than the
 // planner's model (N = 8 rank 7: 0.45-0.70 ms per sample for 340-670 steps).  Same box, N = 8
